@@ -1,0 +1,146 @@
+// perf_test -- the reference's measurement harness (tests/perf_test.cpp:34-158) for the
+// MI355X build, written against the same C ABI (include/mini_nccl_api.h).
+//
+//   perf_test <rank> <n_ranks> [master_ip] [--mode device|staged] [--sizes MiB,MiB,...]
+//
+// Same protocol as the reference: sizes 1/16/64/128 MiB fp32, every rank sends 1.0, 5
+// warm-up and 20 timed all-reduces between CLOCK_MONOTONIC reads, an AVX2 compare scan
+// that every element equals nRanks, and the algbw / busbw table
+// (algbw = bytes / time, busbw = algbw * 2(n-1)/n; perf_test.cpp:140-143).
+//   --mode device  (default) buffers resident in HBM: the headline measurement;
+//   --mode staged  the reference's host-resident buffers (it used cudaHostAlloc,
+//                  perf_test.cpp:78-79): pinned host -> H2D -> all-reduce -> D2H per call,
+//                  i.e. the end-to-end rate including PCIe.
+// Device: rank % device_count (the reference pinned every rank to GPU 0, :46;
+// MINI_NCCL_PERF_DEVICE overrides).
+#include <hip/hip_runtime.h>
+#include <immintrin.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mini_nccl_api.h"
+
+#define HIP_OK(cmd)                                                                             \
+  do {                                                                                          \
+    hipError_t e_ = (cmd);                                                                      \
+    if (e_ != hipSuccess) {                                                                     \
+      fprintf(stderr, "HIP error %s:%d '%s'\n", __FILE__, __LINE__, hipGetErrorString(e_));     \
+      exit(EXIT_FAILURE);                                                                       \
+    }                                                                                           \
+  } while (0)
+
+#define NCCL_OK(cmd)                                                                            \
+  do {                                                                                          \
+    ncclResult_t r_ = (cmd);                                                                    \
+    if (r_ != ncclSuccess) {                                                                    \
+      fprintf(stderr, "mini-nccl error %s:%d '%s'\n", __FILE__, __LINE__, ncclGetErrorString(r_)); \
+      exit(EXIT_FAILURE);                                                                       \
+    }                                                                                           \
+  } while (0)
+
+static double now_us() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+// AVX2 scan: index of the first element != expected, or -1 (perf_test.cpp:105-134)
+static long first_mismatch(const float* p, size_t n, float expected) {
+  const __m256 want = _mm256_set1_ps(expected);
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    const int m = _mm256_movemask_ps(_mm256_cmp_ps(_mm256_loadu_ps(p + i), want, _CMP_NEQ_OQ));
+    if (m) return (long)(i + (size_t)__builtin_ctz((unsigned)m));
+  }
+  for (; i < n; ++i)
+    if (std::fabs(p[i] - expected) > 1e-5f) return (long)i;
+  return -1;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    fprintf(stderr, "Usage: %s <rank> <n_ranks> [master_ip] [--mode device|staged] [--sizes 1,16,64,128]\n", argv[0]);
+    return 1;
+  }
+  const int rank = atoi(argv[1]);
+  const int nranks = atoi(argv[2]);
+  const char* ip = "127.0.0.1";
+  std::string mode = "device";
+  std::vector<size_t> sizes_mib = {1, 16, 64, 128};
+  int iters = 20, warmup = 5;
+  for (int a = 3; a < argc; ++a) {
+    std::string s = argv[a];
+    if (s == "--mode" && a + 1 < argc) mode = argv[++a];
+    else if (s == "--sizes" && a + 1 < argc) {
+      sizes_mib.clear();
+      for (char* t = strtok(argv[++a], ","); t; t = strtok(nullptr, ",")) sizes_mib.push_back(strtoul(t, nullptr, 10));
+    } else if (s == "--iters" && a + 1 < argc) iters = atoi(argv[++a]);
+    else if (s == "--warmup" && a + 1 < argc) warmup = atoi(argv[++a]);
+    else ip = argv[a];
+  }
+  int ndev = 0;
+  HIP_OK(hipGetDeviceCount(&ndev));
+  const char* dv = getenv("MINI_NCCL_PERF_DEVICE");
+  HIP_OK(hipSetDevice(dv ? atoi(dv) : rank % (ndev > 0 ? ndev : 1)));
+
+  ncclComm_t comm;
+  NCCL_OK(ncclCommInitRank(&comm, nranks, rank, ip));
+  hipStream_t stream;
+  HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+
+  if (rank == 0) {
+    printf("\n=== Mini-NCCL (MI355X) Performance Benchmark, %d ranks, %s buffers ===\n", nranks,
+           mode == "device" ? "HBM-resident" : "host-staged (H2D + all-reduce + D2H)");
+    printf("%15s %15s %15s %15s\n", "Size(B)", "Time(us)", "AlgBW(GB/s)", "BusBW(GB/s)");
+  }
+  int failures = 0;
+  for (size_t mib : sizes_mib) {
+    const size_t bytes = mib << 20, count = bytes / sizeof(float);
+    float *h_send = nullptr, *h_recv = nullptr, *d_send = nullptr, *d_recv = nullptr;
+    HIP_OK(hipHostMalloc((void**)&h_send, bytes, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&h_recv, bytes, hipHostMallocDefault));
+    HIP_OK(hipMalloc((void**)&d_send, bytes));
+    HIP_OK(hipMalloc((void**)&d_recv, bytes));
+    for (size_t i = 0; i < count; ++i) h_send[i] = 1.0f;  // perf_test.cpp:82
+    memset(h_recv, 0, bytes);
+    HIP_OK(hipMemcpy(d_send, h_send, bytes, hipMemcpyHostToDevice));
+
+    auto one = [&]() {
+      if (mode == "staged") HIP_OK(hipMemcpyAsync(d_send, h_send, bytes, hipMemcpyHostToDevice, stream));
+      NCCL_OK(ncclAllReduce(d_send, d_recv, count, ncclFloat, ncclSum, comm, stream));
+      if (mode == "staged") HIP_OK(hipMemcpyAsync(h_recv, d_recv, bytes, hipMemcpyDeviceToHost, stream));
+    };
+    for (int i = 0; i < warmup; ++i) one();
+    HIP_OK(hipStreamSynchronize(stream));
+    const double t0 = now_us();
+    for (int i = 0; i < iters; ++i) one();
+    HIP_OK(hipStreamSynchronize(stream));
+    const double t1 = now_us();
+    if (mode != "staged") HIP_OK(hipMemcpy(h_recv, d_recv, bytes, hipMemcpyDeviceToHost));
+
+    const long bad = first_mismatch(h_recv, count, (float)nranks);
+    if (bad >= 0) {
+      printf("[Rank %d] Verification FAILED for size %zu at %ld: %f\n", rank, bytes, bad, h_recv[bad]);
+      ++failures;
+    }
+    const double us = (t1 - t0) / iters;
+    const double alg = (double)bytes / us / 1e3;
+    const double bus = alg * 2.0 * (nranks - 1) / nranks;
+    if (rank == 0) printf("%15zu %15.2f %15.2f %15.2f %s\n", bytes, us, alg, bus, bad >= 0 ? "(FAIL)" : "");
+    fflush(stdout);
+    HIP_OK(hipFree(d_send));
+    HIP_OK(hipFree(d_recv));
+    HIP_OK(hipHostFree(h_send));
+    HIP_OK(hipHostFree(h_recv));
+  }
+  HIP_OK(hipStreamDestroy(stream));
+  NCCL_OK(ncclCommDestroy(comm));
+  return failures ? 2 : 0;
+}

@@ -1,0 +1,309 @@
+#!/usr/bin/env python3
+"""bench.py -- the headline metric: all-reduce algbw (GB/s) on 1 GiB fp32, device-resident.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+One step = one pass of the hot path over one batch of synthetic fp32 input already
+resident in HBM:
+  N = 1  the 1-GPU local reduce of BASELINE.md (a <- a + b over 1 GiB): the scatter-reduce
+         element-wise kernel alone (the reference's all-reduce is a no-op at one rank,
+         mini_nccl.cu:66);
+  N > 1  one ncclAllReduce(send, recv, 268435456, ncclFloat, ncclSum) per rank through the
+         C ABI (one process per GPU, HIP IPC over xGMI), all-ones input as the reference's
+         perf_test (tests/perf_test.cpp:82), result checked == N.
+value = bytes / (time per step), time = max over ranks of K steps between barriers +
+device synchronisation.  rank 0 prints ONE JSON line; diagnostics go to stderr.
+
+roofline: algorithmic HBM bytes of the dominant kernel per launch (3*4 B per
+reduced element; N=1: 3 * 1 GiB; N>1: 3*4*(n-1)*count/n) / its average launch duration,
+measured here with HIP events on the stream the kernel runs on.  traffic: PMC bytes per
+launch from the rocprofv3 pass committed under profiles/ (see profiles/README.md), or null.
+cpu_baseline (rank 0, N = 1 only): the AVX2 host restatement (oracle/ring_oracle.c, the
+reference has no CPU reduce; its AVX2 code is a verify scan) timed on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mini-nccl_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "all-reduce algbw (GB/s) on 1 GiB fp32, device-resident, at 1/2/4/8 MI355X"
+COUNT = 268435456  # 1 GiB of fp32
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle)
+def cpu_baseline(budget_s=12.0):
+    """The host path, timed on this box's cores: AVX2 a += b over the same 1 GiB (the N=1
+    workload), plus the reference's C1 config (2-rank 127.0.0.1 TCP ring, 4 MiB)."""
+    import numpy as np
+
+    import oracle_api as O
+    L = O.load()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    a = np.full(COUNT, 1.0, np.float32)
+    b = np.full(COUNT, 2.0, np.float32)
+    t_start = time.time()
+    t_mt = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, threads, 1)  # first touch / warm
+    iters = max(1, min(10, int((budget_s * 0.45) / max(t_mt, 1e-3))))
+    t_mt = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, threads, iters)
+    t_st = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, 1, 1)
+    ok = L.oracle_verify_avx2(a.ctypes.data, COUNT, float(1.0 + 2.0 * (2 + iters))) == -1
+    del a, b
+    # C1: 2 ranks over loopback TCP, 4 MiB fp32, 128 KiB slices (BASELINE.json configs[0])
+    c1 = None
+    try:
+        import ctypes
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        n_c1, cnt = 2, (4 << 20) // 4
+        bufs = [np.ones(cnt, np.float32) for _ in range(n_c1)]
+        secs = [ctypes.c_double() for _ in range(n_c1)]
+        rcs = [None] * n_c1
+        c1_iters = 20
+
+        def rank(r):
+            rcs[r] = L.oracle_cpu_ring_tcp(r, n_c1, b"127.0.0.1", port, bufs[r].ctypes.data, cnt, 131072, c1_iters,
+                                           ctypes.byref(secs[r]))
+
+        th = [threading.Thread(target=rank, args=(r,)) for r in range(n_c1)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        if all(rc == 0 for rc in rcs):
+            t_c1 = max(x.value for x in secs)
+            c1 = {"config": "2-rank 127.0.0.1 TCP ring, 4 MiB fp32, SLICE 128 KiB, AVX2 adds",
+                  "algbw_GBps": round(cnt * 4 / t_c1 / 1e9, 3), "us_per_allreduce": round(t_c1 * 1e6, 1),
+                  "iters": c1_iters, "threads": n_c1}
+    except Exception as e:  # reported, never fatal
+        log("C1 TCP baseline failed:", e)
+    return {
+        "value": round(COUNT * 4 / t_mt / 1e9, 3),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"a += b over the full 1 GiB fp32 workload, {iters} timed passes after 1 warm pass "
+                  f"(AVX2 _mm256_add_ps, {threads} threads); verify scan {'ok' if ok else 'FAILED'}",
+        "single_thread_GBps": round(COUNT * 4 / t_st / 1e9, 3),
+        "c1_tcp_ring": c1,
+        "wall_s": round(time.time() - t_start, 1),
+    }
+
+
+# ------------------------------------------------------------------ helpers
+def pmc_traffic(key):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/pmc_summary.json)."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        d = json.load(open(p))
+        e = d.get(key)
+        return (e["hbm_bytes_per_launch"], e.get("source")) if e else (None, None)
+    except Exception:
+        return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=20)   # perf_test.cpp:93-99: 20 timed
+    ap.add_argument("--warmup", type=int, default=5)   # perf_test.cpp:86-90: 5 warm-up
+    ap.add_argument("--count", type=int, default=COUNT)
+    ap.add_argument("--algo", choices=["ring", "direct"], default=os.environ.get("MINI_NCCL_ALGO", "ring"))
+    ap.add_argument("--no-alt", action="store_true", help="N>1: skip the second schedule and the RCCL reference")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    n = world
+
+    cpu = None
+    if n == 1 and rank == 0 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline()  # before the GPU is touched
+            log("cpu baseline:", json.dumps(cpu))
+        except Exception as e:
+            log("cpu baseline failed:", e)
+
+    import torch
+    import mini_nccl as M
+    M.load()
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if n > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=n)
+        os.environ.setdefault("MINI_NCCL_PORT", str(int(os.environ.get("MASTER_PORT", "29500")) + 7))
+        os.environ.setdefault("MINI_NCCL_BLOCKING", "0")  # stream-ordered calls, errors checked after
+
+    def barrier_sync():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    stream = torch.cuda.Stream(device=dev)
+    count = args.count
+    nbytes = count * 4
+    result = {"metric": METRIC, "unit": "GB/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+              "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic"}
+
+    def timed(step_fn, k):
+        """K steps between barrier+sync; returns (wall s, mean per-launch event ms)."""
+        starts = [torch.cuda.Event(enable_timing=True) for _ in range(k)]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in range(k)]
+        barrier_sync()
+        t0 = time.perf_counter()
+        for i in range(k):
+            starts[i].record(stream)
+            step_fn()
+            ends[i].record(stream)
+        barrier_sync()
+        wall = time.perf_counter() - t0
+        ev = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / k
+        return wall, ev
+
+    if n == 1:
+        g = torch.Generator(device=dev)
+        g.manual_seed(1234)
+        a = torch.rand(count, device=dev, generator=g, dtype=torch.float32)
+        b = torch.rand(count, device=dev, generator=g, dtype=torch.float32)
+        # parity spot check of one step against torch fp32 (the op is one IEEE add: bit-exact)
+        ref = (a[: 1 << 20] + b[: 1 << 20]).clone()
+        sh = stream.cuda_stream
+
+        def step():
+            rc = M.local_reduce(a.data_ptr(), a.data_ptr(), b.data_ptr(), count, M.ncclFloat, M.ncclSum, sh)
+            if rc != 0:
+                raise M.NcclError(rc, "mncclLocalReduce")
+
+        step()
+        torch.cuda.synchronize()
+        exact = bool(torch.equal(a[: 1 << 20], ref))
+        for _ in range(args.warmup):
+            step()
+        wall, ev_ms = timed(step, args.steps)
+        ms = wall / args.steps * 1e3
+        alg_bytes = 3 * nbytes
+        result.update({
+            "value": round(nbytes / (ms / 1e3) / 1e9, 3),
+            "ms_per_step": round(ms, 4),
+            "config": {"workload": "1-GPU local reduce a <- a + b, 1 GiB fp32 (BASELINE.md row '1-GPU local reduce')",
+                       "count": count, "bytes": nbytes, "kernel": "local_reduce_vec<float,Sum>", "parity_step_exact": exact},
+        })
+        traffic, tsrc = pmc_traffic("local_reduce_f32_1GiB")
+        kern_key = "local_reduce_vec"
+    else:
+        comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
+        info = comm.info()
+        send = torch.ones(count, device=dev, dtype=torch.float32)
+        recv = torch.empty(count, device=dev, dtype=torch.float32)
+        sh = stream.cuda_stream
+
+        def make_step():
+            def step():
+                rc = comm.all_reduce(send.data_ptr(), recv.data_ptr(), count, M.ncclFloat, M.ncclSum, sh)
+                if rc != 0:
+                    raise M.NcclError(rc, "ncclAllReduce")
+            return step
+
+        def run_algo(algo):
+            comm.set_algo(M.ALGO_DIRECT if algo == "direct" else M.ALGO_RING)
+            step = make_step()
+            recv.fill_(-1.0)
+            for _ in range(max(1, args.warmup)):
+                step()
+            torch.cuda.synchronize()
+            ok = bool((recv == float(n)).all().item())  # perf_test.cpp:101-134 known answer
+            wall, ev_ms = timed(step, args.steps)
+            ae = comm.async_error()
+            ok = ok and ae == 0 and bool((recv == float(n)).all().item())
+            ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
+            return max_over_ranks(wall), max_over_ranks(ev_ms), ok
+
+        wall, ev_ms, ok = run_algo(args.algo)
+        ms = wall / args.steps * 1e3
+        algbw = nbytes / (ms / 1e3) / 1e9
+        alg_bytes = 3 * 4 * (n - 1) * (count // n)
+        result.update({
+            "value": round(algbw, 3),
+            "ms_per_step": round(ms, 4),
+            "config": {"workload": f"{n}-rank ring all-reduce, 1 GiB fp32 per rank, HIP IPC over xGMI",
+                       "count": count, "bytes": nbytes, "algo": args.algo, "slice_bytes": info["slice_bytes"],
+                       "channels": info["channels"], "slots": info["slots"], "threads": info["threads"],
+                       "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED"},
+            "busbw": round(algbw * 2 * (n - 1) / n, 3),
+        })
+        if not args.no_alt:
+            other = "direct" if args.algo == "ring" else "ring"
+            try:
+                w2, e2, ok2 = run_algo(other)
+                ms2 = w2 / args.steps * 1e3
+                result["alt"] = {"algo": other, "value": round(nbytes / (ms2 / 1e3) / 1e9, 3), "ms_per_step": round(ms2, 4),
+                                 "kernel_ms": round(e2, 4), "result_check": "ok" if ok2 else "FAILED"}
+            except Exception as e:
+                result["alt"] = {"algo": other, "error": str(e)}
+            comm.set_algo(M.ALGO_DIRECT if args.algo == "direct" else M.ALGO_RING)
+        traffic, tsrc = pmc_traffic(f"{args.algo}_f32_1GiB_n{n}")
+        kern_key = f"{args.algo}_kernel"
+    achieved = alg_bytes / (ev_ms / 1e3) / 1e9
+    result["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                          "kernel": kern_key, "kernel_ms": round(ev_ms, 4), "alg_bytes_per_launch": alg_bytes}
+    if traffic is not None:
+        result["roofline"]["traffic_source"] = tsrc
+    if n > 1 and not args.no_alt:
+        # the comparison ceiling: RCCL's all-reduce on the same buffer (torch.distributed nccl)
+        try:
+            import torch.distributed as dist_
+            pg = dist_.new_group(backend="nccl")
+            x = torch.ones(count, device=dev, dtype=torch.float32)
+            for _ in range(max(1, args.warmup)):
+                dist_.all_reduce(x, group=pg)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                dist_.all_reduce(x, group=pg)
+            torch.cuda.synchronize()
+            dist.barrier()
+            w3 = max_over_ranks(time.perf_counter() - t0)
+            result["rccl_reference"] = {"value": round(nbytes / (w3 / args.steps) / 1e9, 3),
+                                        "ms_per_step": round(w3 / args.steps * 1e3, 4)}
+        except Exception as e:
+            result["rccl_reference"] = {"error": str(e)[:200]}
+    result["cpu_baseline"] = cpu
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if n > 1:
+        comm.destroy()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

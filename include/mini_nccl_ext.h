@@ -1,0 +1,65 @@
+/*
+ * mini_nccl_ext.h -- MI355X-build extensions next to the drop-in ABI.
+ *
+ * Nothing here is needed to use the library as a drop-in for the reference; these
+ * entry points expose the hot path's pieces for measurement and diagnostics:
+ *
+ *   mncclLocalReduce     the ★ scatter-reduce element-wise kernel on its own
+ *                        (reference elementwise_reduce_kernel, mini_nccl.cu:43-47):
+ *                        out[i] = op(local[i], incoming[i]); the 1-GPU "local reduce"
+ *                        workload of BASELINE.md and bench.py at N = 1.
+ *   mncclCommGetAsyncError  sticky error of a communicator (a timed-out or aborted
+ *                        all-reduce leaves the ring state inconsistent; every later
+ *                        call returns this error), like NCCL's ncclCommGetAsyncError.
+ *   mncclCommGetInfo     resolved configuration of a communicator.
+ *   mncclCommSetAlgo     choose the schedule for later calls (same association order).
+ */
+#ifndef MINI_NCCL_EXT_H_
+#define MINI_NCCL_EXT_H_
+
+#include "mini_nccl_api.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* schedules; both produce bit-identical results (same fold order per element) */
+typedef enum {
+  mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
+  mncclAlgoDirect = 1  /* owner of chunk c pulls nothing: every peer pushes its chunk-c slice
+                          straight to c over its own xGMI link; c folds in ring order
+                          c, c+1, ..., c-1 and pushes the result to every peer */
+} mncclAlgo_t;
+
+typedef struct {
+  int rank, nranks, device;
+  size_t slice_bytes;     /* MINI_NCCL_SLICE_SIZE: bytes per channel message */
+  int window;             /* MINI_NCCL_WINDOW_SIZE: messages in flight per link = channels * slots */
+  int signal_batch;       /* MINI_NCCL_SIGNAL_BATCH (read and validated) */
+  int channels;           /* workgroups of the persistent kernel = independent pipelines */
+  int slots;              /* scratch slots per channel (2 = the reference's double buffer) */
+  int threads;            /* threads per workgroup */
+  int algo;               /* mncclAlgo_t used by ncclAllReduce */
+  int blocking;           /* MINI_NCCL_BLOCKING */
+  int sys_fence;          /* MINI_NCCL_SYS_FENCE: system-scope release fence before each flag */
+  double timeout_s;       /* MINI_NCCL_TIMEOUT_MS / 1000 */
+  size_t scratch_bytes;   /* device scratch owned by this rank */
+} mncclCommInfo_t;
+
+ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,
+                              ncclDataType_t datatype, ncclRedOp_t op, hipStream_t stream);
+
+ncclResult_t mncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError);
+
+ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info);
+
+ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo);
+
+/* library version, 10000*major + 100*minor + patch */
+int mncclVersion(void);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* MINI_NCCL_EXT_H_ */

@@ -1,0 +1,171 @@
+// api.cpp -- the C ABI (include/mini_nccl_api.h, include/mini_nccl_ext.h).
+//
+// Thin bridge, as the reference's src/api.cpp: argument checks in the reference's order
+// and with its error codes, an exception firewall (no C++ exception crosses the ABI),
+// dtype/op validation, one roctx range per all-reduce (the reference's NVTX range,
+// api.cpp:142-151), then the communicator's hot path.
+#include <hip/hip_runtime_api.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <cstdio>
+#include <exception>
+#include <new>
+#include <stdexcept>
+#include <string>
+
+#include "comm.h"
+#include "kernels.h"
+#include "mini_nccl_api.h"
+#include "mini_nccl_ext.h"
+
+using mnccl::Comm;
+
+namespace {
+
+// reference api.cpp:101-128: Float/Int32/Double x Sum/Prod/Max/Min; this build adds
+// Float16/Bfloat16 (build-defined parity).  Anything else -> error.
+bool dtype_ok(ncclDataType_t t) {
+  return t == ncclFloat || t == ncclDouble || t == ncclInt32 || t == ncclFloat16 || t == ncclBfloat16;
+}
+bool op_ok(ncclRedOp_t op) { return op == ncclSum || op == ncclProd || op == ncclMax || op == ncclMin; }
+
+struct RoctxRange {
+  explicit RoctxRange(const char* m) { roctxRangePushA(m); }
+  ~RoctxRange() { roctxRangePop(); }
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* ncclGetErrorString(ncclResult_t result) {
+  switch (result) {
+    case ncclSuccess: return "no error";
+    case ncclUnhandledCudaError: return "unhandled hip error";
+    case ncclSystemError: return "system error";
+    case ncclInternalError: return "internal error";
+    case ncclInvalidArgument: return "invalid argument";
+    case ncclInvalidUsage: return "invalid usage";
+    case ncclRemoteError: return "remote error";
+    case ncclInProgress: return "in progress";
+    default: return "unknown error";
+  }
+}
+
+ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nRanks, int rank, const char* ip) {
+  if (!comm) return ncclInvalidArgument;
+  if (rank == -1) {
+    fprintf(stderr, "[Mini-NCCL] Hera auto-rank mode (rank == -1) is not supported by this build\n");
+    return ncclInvalidUsage;
+  }
+  if (nRanks < 1 || rank < 0 || rank >= nRanks) return ncclInvalidArgument;
+  try {
+    Comm* c = new Comm(nRanks, rank, ip ? std::string(ip) : std::string("127.0.0.1"));
+    *comm = reinterpret_cast<ncclComm_t>(c);
+    return ncclSuccess;
+  } catch (const std::invalid_argument& e) {
+    fprintf(stderr, "[Mini-NCCL] Init Failed: %s\n", e.what());
+    return ncclInvalidUsage;
+  } catch (const std::exception& e) {
+    fprintf(stderr, "[Mini-NCCL] Init Failed: %s\n", e.what());
+    return ncclSystemError;
+  } catch (...) {
+    return ncclSystemError;
+  }
+}
+
+ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+  if (!comm) return ncclInvalidArgument;
+  try {
+    delete reinterpret_cast<Comm*>(comm);
+    return ncclSuccess;
+  } catch (...) {
+    return ncclSystemError;
+  }
+}
+
+ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
+  if (!comm || !rank) return ncclInvalidArgument;
+  *rank = reinterpret_cast<const Comm*>(comm)->rank();
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
+  if (!comm || !count) return ncclInvalidArgument;
+  *count = reinterpret_cast<const Comm*>(comm)->nranks();
+  return ncclSuccess;
+}
+
+ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                           ncclRedOp_t op, ncclComm_t comm, hipStream_t stream) {
+  if (!comm || !sendbuff || !recvbuff) return ncclInvalidArgument;  // api.cpp:139
+  if (count == 0) return ncclSuccess;                               // api.cpp:140
+  RoctxRange range("mini_ncclAllReduce");
+  if (!dtype_ok(datatype) || !op_ok(op)) {
+    // the reference throws inside get_type_size / to_internal_op -> ncclInternalError (:182-185)
+    fprintf(stderr, "[Mini-NCCL] AllReduce Internal Error: unsupported %s\n", dtype_ok(datatype) ? "RedOp" : "DataType");
+    return ncclInternalError;
+  }
+  try {
+    return reinterpret_cast<Comm*>(comm)->allreduce(sendbuff, recvbuff, count, (int)datatype, (int)op, stream);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "[Mini-NCCL] AllReduce Internal Error: %s\n", e.what());
+    return ncclInternalError;
+  } catch (...) {
+    return ncclSystemError;
+  }
+}
+
+// ------------------------------------------------------------------ extensions
+ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,
+                              ncclDataType_t datatype, ncclRedOp_t op, hipStream_t stream) {
+  if (!out || !local || !incoming) return ncclInvalidArgument;
+  if (count == 0) return ncclSuccess;
+  if (!dtype_ok(datatype) || !op_ok(op)) return ncclInternalError;
+  try {
+    return mnccl::local_reduce(out, local, incoming, count, (int)datatype, (int)op, stream);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "[Mini-NCCL] LocalReduce Internal Error: %s\n", e.what());
+    return ncclInternalError;
+  } catch (...) {
+    return ncclSystemError;
+  }
+}
+
+ncclResult_t mncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError) {
+  if (!comm || !asyncError) return ncclInvalidArgument;
+  *asyncError = reinterpret_cast<Comm*>(comm)->async_error();
+  return ncclSuccess;
+}
+
+ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info) {
+  if (!comm || !info) return ncclInvalidArgument;
+  const Comm* c = reinterpret_cast<const Comm*>(comm);
+  const mnccl::Config& k = c->config();
+  info->rank = c->rank();
+  info->nranks = c->nranks();
+  info->device = c->device();
+  info->slice_bytes = k.slice_size;
+  info->window = k.window_size;
+  info->signal_batch = k.signal_batch;
+  info->channels = k.channels;
+  info->slots = k.slots;
+  info->threads = k.threads;
+  info->algo = c->algo();
+  info->blocking = k.blocking;
+  info->sys_fence = k.sys_fence;
+  info->timeout_s = k.timeout_ms / 1000.0;
+  info->scratch_bytes = c->scratch_bytes();
+  return ncclSuccess;
+}
+
+ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo) {
+  if (!comm) return ncclInvalidArgument;
+  if (algo != mncclAlgoRing && algo != mncclAlgoDirect) return ncclInvalidArgument;
+  reinterpret_cast<Comm*>(comm)->set_algo(algo);
+  return ncclSuccess;
+}
+
+int mncclVersion(void) { return 100; /* 0.1.0 */ }
+
+}  // extern "C"

@@ -1,0 +1,319 @@
+// comm.cpp -- see comm.h.
+#include "comm.h"
+
+#include <sched.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <stdexcept>
+
+#include "schedule.h"
+
+namespace mnccl {
+
+namespace {
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + what + " : " + hipGetErrorString(e));
+}
+
+double now_s() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+uint64_t host_hash() {
+  char h[256] = {0};
+  gethostname(h, sizeof h - 1);
+  return (uint64_t)std::hash<std::string>{}(std::string(h));
+}
+
+// Record every rank publishes once at init (the reference's RdmaInfo/DynamicMemInfo,
+// RDMATransport.h:25-48, reduced to what one node over HIP IPC needs).
+struct PeerInfo {
+  uint32_t magic;
+  int32_t rank, nranks, pid, device, pad0;
+  uint64_t host;
+  uint64_t slice, scratch_bytes, mbox_bytes;
+  int32_t channels, slots, threads, abi;
+  hipIpcMemHandle_t scratch_h, mbox_h;
+  uint64_t scratch_ptr, mbox_ptr;  // raw addresses for ranks living in the same process
+};
+constexpr uint32_t kInfoMagic = 0x4d4e4931u;  // 'MNI1'
+
+}  // namespace
+
+Comm::Comm(int nranks, int rank, const std::string& ip) : rank_(rank), nranks_(nranks) {
+  cfg_ = Config::from_env();
+  algo_ = cfg_.algo;
+  if (nranks > kMaxRanks) throw std::invalid_argument("nRanks > 16 is not supported on one node");
+  hip_check(hipGetDevice(&device_), "hipGetDevice");
+  if (cfg_.debug && rank == 0) fprintf(stderr, "[Config] Loaded: %s\n", cfg_.describe().c_str());
+  try {
+    setup_device_resources();
+    boot_.connect(rank, nranks, ip, cfg_.port, cfg_.bootstrap_timeout_ms / 1000.0);
+    exchange_and_map();
+  } catch (...) {
+    release();
+    throw;
+  }
+}
+
+void Comm::setup_device_resources() {
+  const int C = cfg_.channels;
+  scratch_bytes_ = (size_t)nranks_ * scratch_region_bytes(C, cfg_.slots, cfg_.slice_size);
+  mbox_bytes_ = (size_t)mbox_words(nranks_, C) * sizeof(uint64_t);
+  if (nranks_ > 1) {
+    hip_check(hipExtMallocWithFlags((void**)&scratch_, scratch_bytes_, hipDeviceMallocUncached), "alloc scratch");
+    hip_check(hipExtMallocWithFlags((void**)&mbox_, mbox_bytes_, hipDeviceMallocUncached), "alloc mailbox");
+    hip_check(hipMemset(scratch_, 0, scratch_bytes_), "memset scratch");
+    hip_check(hipMemset(mbox_, 0, mbox_bytes_), "memset mailbox");
+    const size_t seq_bytes = (size_t)2 * nranks_ * C * sizeof(uint64_t);
+    hip_check(hipMalloc((void**)&pair_seq_, seq_bytes), "alloc pair_seq");
+    hip_check(hipMemset(pair_seq_, 0, seq_bytes), "memset pair_seq");
+  }
+  hip_check(hipHostMalloc((void**)&h_ctl_, 4096, hipHostMallocMapped | hipHostMallocCoherent), "alloc ctl");
+  memset(h_ctl_, 0, 4096);
+  hip_check(hipHostGetDevicePointer((void**)&d_ctl_, h_ctl_, 0), "ctl device pointer");
+  hip_check(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "event");
+  hip_check(hipDeviceSynchronize(), "init sync");
+}
+
+void Comm::exchange_and_map() {
+  peer_scratch_.assign((size_t)nranks_, nullptr);
+  peer_mbox_.assign((size_t)nranks_, nullptr);
+  peer_opened_.assign((size_t)nranks_, false);
+  if (nranks_ == 1) return;
+  PeerInfo me;
+  memset(&me, 0, sizeof me);
+  me.magic = kInfoMagic;
+  me.rank = rank_;
+  me.nranks = nranks_;
+  me.pid = (int32_t)getpid();
+  me.device = device_;
+  me.host = host_hash();
+  me.slice = cfg_.slice_size;
+  me.scratch_bytes = scratch_bytes_;
+  me.mbox_bytes = mbox_bytes_;
+  me.channels = cfg_.channels;
+  me.slots = cfg_.slots;
+  me.threads = cfg_.threads;
+  me.abi = 1;
+  hip_check(hipIpcGetMemHandle(&me.scratch_h, scratch_), "ipc handle scratch");
+  hip_check(hipIpcGetMemHandle(&me.mbox_h, mbox_), "ipc handle mailbox");
+  me.scratch_ptr = (uint64_t)(uintptr_t)scratch_;
+  me.mbox_ptr = (uint64_t)(uintptr_t)mbox_;
+
+  std::vector<PeerInfo> all((size_t)nranks_);
+  boot_.allgather(&me, all.data(), sizeof me);
+  for (int q = 0; q < nranks_; ++q) {
+    const PeerInfo& p = all[(size_t)q];
+    if (p.magic != kInfoMagic || p.rank != q || p.nranks != nranks_)
+      throw std::runtime_error("bootstrap: inconsistent rank records");
+    if (p.host != me.host) throw std::runtime_error("rank " + std::to_string(q) + " is on another host: only one node is supported");
+    if (p.slice != me.slice || p.channels != me.channels || p.slots != me.slots || p.threads != me.threads)
+      throw std::invalid_argument("MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SLOTS / CHANNELS / THREADS differ between ranks");
+  }
+  for (int q = 0; q < nranks_; ++q) {
+    if (q == rank_) {
+      peer_scratch_[(size_t)q] = scratch_;
+      peer_mbox_[(size_t)q] = mbox_;
+      continue;
+    }
+    const PeerInfo& p = all[(size_t)q];
+    if (p.pid == me.pid) {  // same process (e.g. threads of one test): plain pointers
+      peer_scratch_[(size_t)q] = (char*)(uintptr_t)p.scratch_ptr;
+      peer_mbox_[(size_t)q] = (uint64_t*)(uintptr_t)p.mbox_ptr;
+      continue;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) == hipSuccess && p.device != device_ && p.device < ndev) {
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, device_, p.device) == hipSuccess && can) {
+        hipError_t e = hipDeviceEnablePeerAccess(p.device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+      }
+    }
+    void* ps = nullptr;
+    void* pm = nullptr;
+    hip_check(hipIpcOpenMemHandle(&ps, p.scratch_h, hipIpcMemLazyEnablePeerAccess), "ipc open scratch");
+    hip_check(hipIpcOpenMemHandle(&pm, p.mbox_h, hipIpcMemLazyEnablePeerAccess), "ipc open mailbox");
+    peer_scratch_[(size_t)q] = (char*)ps;
+    peer_mbox_[(size_t)q] = (uint64_t*)pm;
+    peer_opened_[(size_t)q] = true;
+  }
+  // every rank has mapped every peer and its own memory is zeroed before anyone writes
+  boot_.barrier();
+}
+
+Comm::~Comm() {
+  hipSetDevice(device_);
+  if (done_) hipEventSynchronize(done_);
+  if (nranks_ > 1 && !peer_scratch_.empty()) {
+    try {
+      if (sticky_ == ncclSuccess) boot_.barrier();  // nobody still writes into my memory
+    } catch (...) {
+    }
+    for (int q = 0; q < nranks_; ++q) {
+      if (peer_opened_[(size_t)q]) {
+        hipIpcCloseMemHandle(peer_scratch_[(size_t)q]);
+        hipIpcCloseMemHandle(peer_mbox_[(size_t)q]);
+        peer_opened_[(size_t)q] = false;
+      }
+    }
+    try {
+      if (sticky_ == ncclSuccess) boot_.barrier();  // nobody still maps my memory
+    } catch (...) {
+    }
+  }
+  release();
+}
+
+void Comm::release() {
+  for (int q = 0; q < (int)peer_opened_.size(); ++q) {
+    if (peer_opened_[(size_t)q]) {
+      hipIpcCloseMemHandle(peer_scratch_[(size_t)q]);
+      hipIpcCloseMemHandle(peer_mbox_[(size_t)q]);
+      peer_opened_[(size_t)q] = false;
+    }
+  }
+  boot_.close_all();
+  if (scratch_) hipFree(scratch_);
+  if (mbox_) hipFree(mbox_);
+  if (pair_seq_) hipFree(pair_seq_);
+  if (h_ctl_) hipHostFree(h_ctl_);
+  if (done_) hipEventDestroy(done_);
+  scratch_ = nullptr;
+  mbox_ = nullptr;
+  pair_seq_ = nullptr;
+  h_ctl_ = nullptr;
+  done_ = nullptr;
+  (void)hipGetLastError();
+}
+
+ncclResult_t Comm::check_status() {
+  const uint32_t st = __atomic_load_n(&h_ctl_[0], __ATOMIC_ACQUIRE);
+  if (st == 0) return ncclSuccess;
+  if (sticky_ == ncclSuccess) {
+    sticky_ = (st & kStatusRemoteAbort) && !(st & kStatusTimeout) ? ncclRemoteError : ncclInternalError;
+    fprintf(stderr, "[Mini-NCCL] rank %d: all-reduce %s (status 0x%x); communicator is no longer usable\n", rank_,
+            (st & kStatusTimeout) ? "timed out (watchdog)" : (st & kStatusHostAbort) ? "aborted by host" : "aborted by a peer",
+            st);
+  }
+  return sticky_;
+}
+
+ncclResult_t Comm::async_error() {
+  if (sticky_ != ncclSuccess) return sticky_;
+  if (h_ctl_) return check_status();
+  return ncclSuccess;
+}
+
+// Host side of the reference's watchdog (mini_nccl.cu:200-214): wait for the stream; after
+// the kernel's own timeout plus a grace period, raise the abort word the kernel polls.
+ncclResult_t Comm::wait_for(hipStream_t stream) {
+  hip_check(hipEventRecord(done_, stream), "event record");
+  const double t0 = now_s();
+  const double limit = cfg_.timeout_ms / 1000.0 + 2.0;
+  bool aborted = false;
+  for (int spins = 0;; ++spins) {
+    hipError_t q = hipEventQuery(done_);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) hip_check(q, "stream query");
+    const double el = now_s() - t0;
+    if (!aborted && el > limit) {
+      fprintf(stderr, "[Watchdog] TIMEOUT DETECTED on rank %d! Aborting GPU kernels...\n", rank_);
+      __atomic_store_n(&h_ctl_[1], 1u, __ATOMIC_RELEASE);
+      aborted = true;
+    }
+    if (aborted && el > limit + 10.0) {
+      sticky_ = ncclInternalError;
+      return sticky_;
+    }
+    if (spins < 2000) sched_yield();
+    else usleep(el < 0.01 ? 10 : 100);
+  }
+  return check_status();
+}
+
+ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t stream) {
+  if (sticky_ != ncclSuccess) return sticky_;
+  if (check_status() != ncclSuccess) return sticky_;
+  const int esz = dtype_size(dtype);
+  const size_t bytes = count * (size_t)esz;
+  int cur_dev = -1;
+  hip_check(hipGetDevice(&cur_dev), "hipGetDevice");
+  if (cur_dev != device_) hip_check(hipSetDevice(device_), "hipSetDevice");
+
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cap) != hipSuccess) {
+    (void)hipGetLastError();
+    cap = hipStreamCaptureStatusNone;
+  }
+  if (cap == hipStreamCaptureStatusActive && !warned_capture_) {
+    // the reference warns here too (api.cpp:153-166); this build needs no host polling,
+    // so a captured all-reduce replays correctly (sequence state lives on the device)
+    if (cfg_.debug) fprintf(stderr, "[Mini-NCCL] HIP graph capture detected: host-side wait skipped\n");
+    warned_capture_ = true;
+  }
+
+  const int n = nranks_;
+  const size_t chunk = n > 0 ? count / (size_t)n : 0;  // mini_nccl.cu:69
+  const size_t chunk_bytes = chunk * (size_t)esz;
+  if (n == 1 || chunk == 0) {
+    // nRanks == 1 returns after the copy (mini_nccl.cu:66); chunk == 0 moves no slice
+    if (send != recv) hip_check(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, stream), "copy");
+  } else {
+    // elements past n*chunk keep this rank's own input (the reference copies the whole
+    // buffer and never touches the tail, api.cpp:173-175 + mini_nccl.cu:69); the ring
+    // writes every other element of recv, so only the tail needs the copy
+    const size_t body = chunk_bytes * (size_t)n;
+    if (send != recv && bytes > body)
+      hip_check(hipMemcpyAsync((char*)recv + body, (const char*)send + body, bytes - body, hipMemcpyDeviceToDevice,
+                               stream),
+                "tail copy");
+    CollParams p;
+    memset(&p, 0, sizeof p);
+    p.send = (const char*)send;
+    p.recv = (char*)recv;
+    p.chunk_bytes = chunk_bytes;
+    p.slice_bytes = cfg_.slice_size;
+    p.nslices = (chunk_bytes + cfg_.slice_size - 1) / cfg_.slice_size;
+    const int C = cfg_.channels;
+    p.iters = (uint32_t)((p.nslices + (uint64_t)C - 1) / (uint64_t)C);
+    p.n = n;
+    p.rank = rank_;
+    p.nslots = cfg_.slots;
+    p.scratch = scratch_;
+    p.mbox = mbox_;
+    p.tx_seq = pair_seq_;
+    p.rx_seq = pair_seq_ + (size_t)n * C;
+    for (int q = 0; q < n; ++q) {
+      p.peer_scratch[q] = peer_scratch_[(size_t)q];
+      p.peer_mbox[q] = peer_mbox_[(size_t)q];
+    }
+    p.status = d_ctl_;
+    p.host_abort = d_ctl_ + 1;
+    p.timeout_ticks = (uint64_t)(cfg_.timeout_ms * 1e5);  // s_memrealtime runs at 100 MHz
+    p.sys_fence = cfg_.sys_fence;
+    const bool vec = (((uintptr_t)send | (uintptr_t)recv) % 16 == 0) && (chunk_bytes % 16 == 0);
+    hipError_t e = algo_ == 1 ? launch_direct(dtype, op, vec, C, cfg_.threads, p, stream)
+                              : launch_ring(dtype, op, vec, C, cfg_.threads, p, stream);
+    hip_check(e, "kernel launch");
+  }
+  if (cur_dev != device_) hipSetDevice(cur_dev);
+  if (cfg_.blocking && cap == hipStreamCaptureStatusNone) return wait_for(stream);
+  return ncclSuccess;
+}
+
+ncclResult_t local_reduce(void* out, const void* local, const void* incoming, size_t count, int dtype, int op,
+                          hipStream_t stream) {
+  hip_check(launch_local_reduce(dtype, op, out, local, incoming, count, stream), "local reduce launch");
+  return ncclSuccess;
+}
+
+}  // namespace mnccl

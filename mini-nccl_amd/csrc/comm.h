@@ -1,0 +1,71 @@
+// comm.h -- the communicator behind ncclComm_t (reference: Context + RDMATransport,
+// include/mini_nccl.h:71-111 and src/transport/RDMATransport.h:99-637, re-designed for one
+// MI355X node: HIP IPC over xGMI instead of verbs, device scratch instead of host-mapped).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "bootstrap.h"
+#include "config.h"
+#include "kernels.h"
+#include "mini_nccl_api.h"
+
+namespace mnccl {
+
+class Comm {
+ public:
+  // Throws on failure; the API layer maps exceptions to ncclSystemError (api.cpp:62-65).
+  Comm(int nranks, int rank, const std::string& ip);
+  ~Comm();
+  Comm(const Comm&) = delete;
+  Comm& operator=(const Comm&) = delete;
+
+  // The hot path: returns an ncclResult_t; throws only on HIP runtime errors.
+  ncclResult_t allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t stream);
+
+  int rank() const { return rank_; }
+  int nranks() const { return nranks_; }
+  int device() const { return device_; }
+  const Config& config() const { return cfg_; }
+  int algo() const { return algo_; }
+  void set_algo(int a) { algo_ = a; }
+  ncclResult_t async_error();
+  size_t scratch_bytes() const { return scratch_bytes_; }
+
+ private:
+  void setup_device_resources();
+  void release();
+  void exchange_and_map();
+  ncclResult_t wait_for(hipStream_t stream);
+  ncclResult_t check_status();
+
+  int rank_, nranks_, device_ = 0;
+  Config cfg_;
+  int algo_ = 0;
+  Bootstrap boot_;
+
+  char* scratch_ = nullptr;      // uncached device memory, peers write into it
+  size_t scratch_bytes_ = 0;
+  uint64_t* mbox_ = nullptr;     // uncached device memory: READY / CREDIT / ABORT words
+  size_t mbox_bytes_ = 0;
+  uint64_t* pair_seq_ = nullptr; // [2][n][C]: per (peer, channel) tx / rx message counters (device)
+  uint32_t* h_ctl_ = nullptr;    // host-mapped: [0] status, [1] abort request
+  uint32_t* d_ctl_ = nullptr;    // device view of h_ctl_
+
+  std::vector<char*> peer_scratch_;
+  std::vector<uint64_t*> peer_mbox_;
+  std::vector<bool> peer_opened_;  // true: mapped with hipIpcOpenMemHandle (close on destroy)
+
+  hipEvent_t done_ = nullptr;
+  ncclResult_t sticky_ = ncclSuccess;
+  bool warned_capture_ = false;
+};
+
+// 1-GPU local reduce (mini_nccl_ext.h): no communicator needed.
+ncclResult_t local_reduce(void* out, const void* local, const void* incoming, size_t count, int dtype, int op,
+                          hipStream_t stream);
+
+}  // namespace mnccl

@@ -1,0 +1,75 @@
+// config.cpp -- see config.h.
+#include "config.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace mnccl {
+
+namespace {
+
+long long env_int(const char* name, long long dflt) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  char* end = nullptr;
+  long long x = std::strtoll(v, &end, 0);
+  if (end == v || *end) throw std::invalid_argument(std::string(name) + "=" + v + " is not an integer");
+  return x;
+}
+
+}  // namespace
+
+Config Config::from_env() {
+  Config c;
+  long long slice = env_int("MINI_NCCL_SLICE_SIZE", 128 * 1024);
+  if (slice <= 0) slice = 1024;  // Config.h:50 maps 0 -> 1024
+  slice &= ~15LL;                // whole 16-byte vectors per message (slicing never changes results)
+  if (slice < 16) slice = 16;
+  c.slice_size = (size_t)slice;
+  c.window_size = (int)env_int("MINI_NCCL_WINDOW_SIZE", 64);
+  if (c.window_size <= 0) c.window_size = 1;  // Config.h:51
+  c.signal_batch = (int)env_int("MINI_NCCL_SIGNAL_BATCH", 16);
+  if (c.signal_batch <= 0) c.signal_batch = 1;
+  c.slots = (int)env_int("MINI_NCCL_SLOTS", 2);
+  // >= 2: with one slot, op k of a rank would wait for its neighbour's op k (the credit for
+  // the message it is about to overwrite) -- a cycle; tests/test_schedule.py shows it
+  if (c.slots < 2) c.slots = 2;
+  if (c.slots > 64) c.slots = 64;
+  c.channels = (int)env_int("MINI_NCCL_CHANNELS", 0);
+  if (c.channels <= 0) c.channels = c.window_size / c.slots;
+  if (c.channels < 1) c.channels = 1;
+  if (c.channels > 256) c.channels = 256;
+  c.threads = (int)env_int("MINI_NCCL_THREADS", 512);
+  if (c.threads < 64) c.threads = 64;
+  if (c.threads > 1024) c.threads = 1024;
+  c.threads &= ~63;
+  const char* a = std::getenv("MINI_NCCL_ALGO");
+  if (a && *a) {
+    if (!strcmp(a, "ring")) c.algo = 0;
+    else if (!strcmp(a, "direct")) c.algo = 1;
+    else throw std::invalid_argument(std::string("MINI_NCCL_ALGO=") + a + " (expected ring|direct)");
+  }
+  c.blocking = env_int("MINI_NCCL_BLOCKING", 1) != 0;
+  c.sys_fence = env_int("MINI_NCCL_SYS_FENCE", 1) != 0;
+  c.timeout_ms = (double)env_int("MINI_NCCL_TIMEOUT_MS", 10000);
+  if (c.timeout_ms < 1) c.timeout_ms = 1;
+  c.port = (int)env_int("MINI_NCCL_PORT", 8888);
+  c.bootstrap_timeout_ms = (double)env_int("MINI_NCCL_BOOTSTRAP_TIMEOUT_MS", 60000);
+  c.debug = (int)env_int("MINI_NCCL_DEBUG", 0);
+  return c;
+}
+
+std::string Config::describe() const {
+  char b[320];
+  snprintf(b, sizeof b,
+           "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, algo=%s, blocking=%d, "
+           "sys_fence=%d, timeout=%.0f ms, port=%d",
+           slice_size, window_size, signal_batch, slots, channels, threads, algo ? "direct" : "ring", blocking,
+           sys_fence, timeout_ms, port);
+  return b;
+}
+
+}  // namespace mnccl

@@ -1,0 +1,31 @@
+// config.h -- environment knobs (reference include/Config.h:9-62), resolved once per
+// communicator (the scratch ring is sized from them at init, as the reference sizes its
+// scratch at Context construction, mini_nccl.cu:14-20).
+#pragma once
+#include <stddef.h>
+#include <string>
+
+namespace mnccl {
+
+struct Config {
+  // reference knobs, same names and defaults (Config.h:29-51)
+  size_t slice_size = 128 * 1024;  // MINI_NCCL_SLICE_SIZE (bytes per channel message; 0 -> 1024)
+  int window_size = 64;            // MINI_NCCL_WINDOW_SIZE (messages in flight per link)
+  int signal_batch = 16;           // MINI_NCCL_SIGNAL_BATCH (validated)
+  // this build's knobs
+  int slots = 2;                   // MINI_NCCL_SLOTS   scratch slots per channel (>= 2; 2 = double buffer)
+  int channels = 0;                // MINI_NCCL_CHANNELS (0 -> window_size / slots)
+  int threads = 512;               // MINI_NCCL_THREADS threads per workgroup
+  int algo = 0;                    // MINI_NCCL_ALGO    ring | direct
+  int blocking = 1;                // MINI_NCCL_BLOCKING host waits for the stream (reference behaviour)
+  int sys_fence = 1;               // MINI_NCCL_SYS_FENCE system release fence before each flag
+  double timeout_ms = 10000.0;     // MINI_NCCL_TIMEOUT_MS (reference watchdog: 10 s)
+  int port = 8888;                 // MINI_NCCL_PORT   bootstrap port (reference: 8888)
+  double bootstrap_timeout_ms = 60000.0;  // MINI_NCCL_BOOTSTRAP_TIMEOUT_MS
+  int debug = 0;                   // MINI_NCCL_DEBUG
+
+  static Config from_env();
+  std::string describe() const;
+};
+
+}  // namespace mnccl

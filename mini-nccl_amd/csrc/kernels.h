@@ -1,0 +1,48 @@
+// kernels.h -- host-side view of the HIP kernels in kernels.hip (launch wrappers only).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace mnccl {
+
+// Element types the kernels are instantiated for (subset of ncclDataType_t values).
+enum DType : int { kI32 = 2, kF16 = 6, kF32 = 7, kF64 = 8, kBF16 = 9 };
+enum RedOp : int { kSum = 0, kProd = 1, kMax = 2, kMin = 3 };
+
+// Everything a ring / direct kernel needs; passed by value as the kernel argument.
+struct CollParams {
+  const char* send;        // this rank's input (device)
+  char* recv;              // this rank's output (device; may equal send)
+  uint64_t chunk_bytes;    // (count / n) * elem_size
+  uint64_t slice_bytes;    // bytes per channel message
+  uint64_t nslices;        // ceil(chunk_bytes / slice_bytes)
+  uint32_t iters;          // ceil(nslices / channels): slices per channel
+  int32_t n, rank, nslots;
+  char* scratch;           // this rank's scratch (regions per source rank)
+  uint64_t* mbox;          // this rank's mailbox
+  uint64_t* tx_seq;        // [peer][channel] messages sent so far (device, private)
+  uint64_t* rx_seq;        // [peer][channel] messages received so far (device, private)
+  char* peer_scratch[16];  // peers' scratch bases (IPC-mapped), indexed by rank
+  uint64_t* peer_mbox[16]; // peers' mailboxes (IPC-mapped), indexed by rank
+  uint32_t* status;        // host-mapped status word (kStatus* bits)
+  const uint32_t* host_abort;  // host-mapped abort request
+  uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
+  int32_t sys_fence;       // system-scope release fence before each ready flag
+};
+
+constexpr int kMaxRanks = 16;
+
+// Launchers return hipSuccess or the launch error; dtype/op must be supported
+// (checked by the caller).  vec = 16-byte path (all offsets 16-byte aligned).
+hipError_t launch_ring(int dtype, int op, bool vec, int channels, int threads,
+                       const CollParams& p, hipStream_t stream);
+hipError_t launch_direct(int dtype, int op, bool vec, int channels, int threads,
+                         const CollParams& p, hipStream_t stream);
+// out[i] = op(local[i], incoming[i]) for i < count
+hipError_t launch_local_reduce(int dtype, int op, void* out, const void* local,
+                               const void* incoming, uint64_t count, hipStream_t stream);
+
+bool dtype_supported(int dtype);
+int dtype_size(int dtype);
+
+}  // namespace mnccl

@@ -1,0 +1,621 @@
+// kernels.hip -- the hot path, hand-written for CDNA4 (gfx950).
+//
+//  ring_kernel    persistent ring all-reduce (reference mini_nccl.cu:56-217 re-designed):
+//                 one workgroup per channel, each an independent slice pipeline; the
+//                 reference's per-slice launches of wait_kernel (:22-30),
+//                 elementwise_reduce_kernel (:43-47), the IPC memcpy (:131,:174) and
+//                 set_flag_kernel (:32-36) become one launch per call in which every
+//                 channel moves its slices through a `slots`-deep FIFO in the next
+//                 rank's scratch with epoch-free monotone flags and explicit credits.
+//  direct_kernel  same association order, every peer link at once (schedule.h).
+//  local_reduce   the element-wise op alone: out = op(local, incoming), 16 B per lane.
+//
+// Memory-ordering protocol (cross-process, cross-device over xGMI):
+//  * everything another rank writes lives in THIS rank's scratch / mailbox, allocated
+//    hipDeviceMallocUncached: no cache of any agent keeps a copy of those lines;
+//  * payload stores to a peer's slot are system-coherent (sc0 sc1) 16-byte buffer
+//    stores; every storing wave drains (s_waitcnt vmcnt(0)), the workgroup barriers,
+//    lane 0 optionally issues a system-scope release fence, drains again (asm, so the
+//    compiler cannot drop it) and stores the READY word with a system-scope atomic;
+//  * the consumer polls its own READY word with system-scope relaxed loads from one
+//    lane (s_sleep between polls), then one system-scope acquire fence, a barrier, and
+//    reads the slot with sc0 sc1 loads (which bypass L1/L2 regardless of mapping);
+//  * after the barrier that follows the last load of a slot, lane 0 returns a CREDIT to
+//    the sender; the sender reuses a slot only after the credit for the message that
+//    last used it (seq - slots) arrived.
+//  * flags are monotone 64-bit sequence numbers that continue across calls (per-channel
+//    base kept in device memory and advanced by the kernel itself, so graph replays stay
+//    consistent); nothing is reset per call and stale flags cannot satisfy a wait.
+//  * every spin is bounded (MINI_NCCL_TIMEOUT_MS via s_memrealtime) and also exits on
+//    the host abort word or a peer's ABORT; the kernel always terminates.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "kernels.h"
+#include "schedule.h"
+
+namespace mnccl {
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef uint64_t u64;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr int kAuxSys = 17;  // sc0 | sc1: system-coherent buffer access
+
+struct bf16_t { uint16_t v; };
+
+// ---------------------------------------------------------------- element ops
+// c = op(a = local, b = incoming), reference mini_nccl.cu:38-41
+template <typename T, int OPC> struct Op;
+template <typename T> struct Op<T, kSum> { __device__ static T f(T a, T b) { return a + b; } };
+template <typename T> struct Op<T, kProd> { __device__ static T f(T a, T b) { return a * b; } };
+template <typename T> struct Op<T, kMax> { __device__ static T f(T a, T b) { return (a > b) ? a : b; } };
+template <typename T> struct Op<T, kMin> { __device__ static T f(T a, T b) { return (a < b) ? a : b; } };
+// int32 +,*: two's-complement wrap (no signed-overflow UB)
+template <> struct Op<int32_t, kSum> {
+  __device__ static int32_t f(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+};
+template <> struct Op<int32_t, kProd> {
+  __device__ static int32_t f(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+};
+// bf16: widen (exact), op in f32, round to nearest even (correctly rounded: 24 >= 2*8+2);
+// NaN -> quiet NaN keeping the high payload bits (same rule as the oracle)
+__device__ __forceinline__ float bf2f(bf16_t x) { return __uint_as_float((uint32_t)x.v << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  bf16_t r;
+  if ((u & 0x7fffffffu) > 0x7f800000u) r.v = (uint16_t)((u >> 16) | 0x40u);
+  else r.v = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  return r;
+}
+template <> struct Op<bf16_t, kSum> { __device__ static bf16_t f(bf16_t a, bf16_t b) { return f2bf(bf2f(a) + bf2f(b)); } };
+template <> struct Op<bf16_t, kProd> { __device__ static bf16_t f(bf16_t a, bf16_t b) { return f2bf(bf2f(a) * bf2f(b)); } };
+template <> struct Op<bf16_t, kMax> { __device__ static bf16_t f(bf16_t a, bf16_t b) { return (bf2f(a) > bf2f(b)) ? a : b; } };
+template <> struct Op<bf16_t, kMin> { __device__ static bf16_t f(bf16_t a, bf16_t b) { return (bf2f(a) < bf2f(b)) ? a : b; } };
+
+template <typename T> struct alignas(16) Pack16 { T x[16 / sizeof(T)]; };
+
+template <typename T, int OPC>
+__device__ __forceinline__ v4u reduce16(v4u a, v4u b) {
+  Pack16<T> pa = __builtin_bit_cast(Pack16<T>, a);
+  const Pack16<T> pb = __builtin_bit_cast(Pack16<T>, b);
+#pragma unroll
+  for (int i = 0; i < (int)(16 / sizeof(T)); ++i) pa.x[i] = Op<T, OPC>::f(pa.x[i], pb.x[i]);
+  return __builtin_bit_cast(v4u, pa);
+}
+
+// ---------------------------------------------------------------- memory primitives
+__device__ __forceinline__ u64 ld_sys(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t ld_sys32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(u64* p, u64 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ v4u ld_slot16(rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxSys);
+}
+__device__ __forceinline__ void st_slot16(rsrc_t r, uint32_t off, v4u v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSys);
+}
+__device__ __forceinline__ v4u ld_g16(const char* p) { return *reinterpret_cast<const v4u*>(p); }
+__device__ __forceinline__ void st_g16(char* p, v4u v) { *reinterpret_cast<v4u*>(p) = v; }
+
+// scalar (unaligned-count) path: one element per access
+template <int SZ> struct Scal;
+template <> struct Scal<2> {
+  typedef uint16_t U;
+  __device__ static U ld(rsrc_t r, uint32_t o) { return __builtin_amdgcn_raw_buffer_load_b16(r, o, 0, kAuxSys); }
+  __device__ static void st(rsrc_t r, uint32_t o, U v) { __builtin_amdgcn_raw_buffer_store_b16(v, r, o, 0, kAuxSys); }
+};
+template <> struct Scal<4> {
+  typedef uint32_t U;
+  __device__ static U ld(rsrc_t r, uint32_t o) { return __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, kAuxSys); }
+  __device__ static void st(rsrc_t r, uint32_t o, U v) { __builtin_amdgcn_raw_buffer_store_b32(v, r, o, 0, kAuxSys); }
+};
+template <> struct Scal<8> {
+  typedef u64 U;
+  __device__ static U ld(rsrc_t r, uint32_t o) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, kAuxSys);
+    return __builtin_bit_cast(U, v);
+  }
+  __device__ static void st(rsrc_t r, uint32_t o, U v) {
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), r, o, 0, kAuxSys);
+  }
+};
+
+// ---------------------------------------------------------------- bounded waits
+struct Ctl {
+  uint32_t* status;
+  const uint32_t* host_abort;
+  const u64* my_abort;
+  uint64_t timeout_ticks;
+};
+
+// lane-0 spin until *flag >= target; false on timeout / abort (status already set)
+__device__ __noinline__ bool wait_ge(const u64* flag, u64 target, const Ctl& c) {
+  if (ld_sys(flag) >= target) return true;
+  const u64 t0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t polls = 1;; ++polls) {
+    __builtin_amdgcn_s_sleep(1);
+    if (ld_sys(flag) >= target) return true;
+    if ((polls & 63) == 0) {
+      if (ld_sys(c.my_abort) != 0) { st_sys32(c.status, kStatusRemoteAbort); return false; }
+      if (ld_sys32(c.host_abort) != 0) { st_sys32(c.status, kStatusHostAbort); return false; }
+      if (ld_sys32(c.status) != 0) return false;  // a sibling workgroup gave up
+      if (__builtin_amdgcn_s_memrealtime() - t0 > c.timeout_ticks) { st_sys32(c.status, kStatusTimeout); return false; }
+    }
+  }
+}
+
+__device__ __forceinline__ void acquire_sys() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+
+// every storing wave: drain its stores (asm so the compiler cannot elide it)
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// lane 0, after the workgroup barrier that follows every wave's drain
+__device__ __forceinline__ void publish(u64* flag, u64 v, int sys_fence) {
+  if (sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  st_sys(flag, v);
+}
+
+// ---------------------------------------------------------------- message bodies
+enum : int { kHasLocal = 1, kHasIn = 2, kWritesRecv = 4, kSends = 8, kReduces = 16 };
+template <int KIND> struct KindBits;
+template <> struct KindBits<kSend> { static constexpr int v = kHasLocal | kSends; };
+template <> struct KindBits<kReduceSend> { static constexpr int v = kHasLocal | kHasIn | kSends | kReduces; };
+template <> struct KindBits<kReduceCopySend> { static constexpr int v = kHasLocal | kHasIn | kSends | kReduces | kWritesRecv; };
+template <> struct KindBits<kCopySend> { static constexpr int v = kHasIn | kSends | kWritesRecv; };
+template <> struct KindBits<kCopy> { static constexpr int v = kHasIn | kWritesRecv; };
+
+constexpr int kU = 4;  // 16-byte vectors per lane per sub-block (4 KB .. 16 KB per sub-block)
+
+template <typename T, int OPC, int KIND>
+__device__ __forceinline__ void move_vec(const char* __restrict__ lsrc, char* __restrict__ ldst, rsrc_t in,
+                                         rsrc_t out, uint32_t nbytes, int tid, int nt) {
+  constexpr int B = KindBits<KIND>::v;
+  const uint32_t nvec = nbytes >> 4;
+  for (uint32_t b = 0; b < nvec; b += (uint32_t)nt * kU) {
+    v4u l[kU], x[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t i = b + (uint32_t)(u * nt + tid);
+      if (i < nvec) {
+        if (B & kHasLocal) l[u] = ld_g16(lsrc + (size_t)i * 16);
+        if (B & kHasIn) x[u] = ld_slot16(in, i * 16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t i = b + (uint32_t)(u * nt + tid);
+      if (i < nvec) {
+        v4u v;
+        if (B & kReduces) v = reduce16<T, OPC>(l[u], x[u]);
+        else if (B & kHasIn) v = x[u];
+        else v = l[u];
+        if (B & kWritesRecv) st_g16(ldst + (size_t)i * 16, v);
+        if (B & kSends) st_slot16(out, i * 16, v);
+      }
+    }
+  }
+}
+
+template <typename T, int OPC, int KIND>
+__device__ __forceinline__ void move_scalar(const char* __restrict__ lsrc, char* __restrict__ ldst, rsrc_t in,
+                                            rsrc_t out, uint32_t nbytes, int tid, int nt) {
+  constexpr int B = KindBits<KIND>::v;
+  typedef typename Scal<sizeof(T)>::U U;
+  const uint32_t ne = nbytes / sizeof(T);
+  for (uint32_t i = tid; i < ne; i += nt) {
+    U l = 0, x = 0, v;
+    if (B & kHasLocal) l = reinterpret_cast<const U*>(lsrc)[i];
+    if (B & kHasIn) x = Scal<sizeof(T)>::ld(in, i * (uint32_t)sizeof(T));
+    if (B & kReduces) v = __builtin_bit_cast(U, Op<T, OPC>::f(__builtin_bit_cast(T, l), __builtin_bit_cast(T, x)));
+    else if (B & kHasIn) v = x;
+    else v = l;
+    if (B & kWritesRecv) reinterpret_cast<U*>(ldst)[i] = v;
+    if (B & kSends) Scal<sizeof(T)>::st(out, i * (uint32_t)sizeof(T), v);
+  }
+}
+
+template <typename T, int OPC, bool VEC, int KIND>
+__device__ __forceinline__ void move(const char* lsrc, char* ldst, rsrc_t in, rsrc_t out, uint32_t nbytes, int tid,
+                                     int nt) {
+  if (VEC) move_vec<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, tid, nt);
+  else move_scalar<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, tid, nt);
+}
+
+__device__ __forceinline__ void abort_peers(const CollParams& p, const int* peers, int npeers) {
+  const int C = gridDim.x;
+  for (int k = 0; k < npeers; ++k) st_sys(p.peer_mbox[peers[k]] + mbox_abort(p.n, C), 1ull);
+}
+
+// ---------------------------------------------------------------- ring kernel
+template <typename T, int OPC, bool VEC>
+__global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
+  const int w = blockIdx.x, C = gridDim.x, tid = threadIdx.x, nt = blockDim.x;
+  const int n = p.n, r = p.rank, K = p.nslots;
+  const int prev = mod_n(r - 1, n), next = mod_n(r + 1, n);
+  __shared__ int s_abort;
+  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks};
+  // per-pair message counters: the FIFO to `next` and the FIFO from `prev` on this channel
+  u64* tx_ctr = p.tx_seq + (u64)next * C + w;
+  u64* rx_ctr = p.rx_seq + (u64)prev * C + w;
+  const u64 tx_base = *tx_ctr, rx_base = *rx_ctr;
+  const int mpi = ring_msgs_per_iter(n);
+  const u64* my_ready = p.mbox + mbox_ready(C, prev, w);
+  const u64* my_credit = p.mbox + mbox_credit(n, C, next, w);
+  u64* out_ready = p.peer_mbox[next] + mbox_ready(C, r, w);
+  u64* out_credit = p.peer_mbox[prev] + mbox_credit(n, C, r, w);
+  const int nops = ring_num_ops(n);
+
+  for (uint32_t it = 0; it < p.iters; ++it) {
+    const u64 s = (u64)it * C + w;
+    const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
+    const u64 soff = s * p.slice_bytes;
+    const u64 itoff = (u64)it * mpi;
+    for (int k = 0; k < nops; ++k) {
+      const RingOp o = ring_op(n, r, k);
+      const u64 rseq = rx_base + itoff + (u64)o.recv_msg, sseq = tx_base + itoff + (u64)o.send_msg;
+      if (tid == 0) {
+        bool ok = true;
+        if (o.recv_msg >= 0) ok = wait_ge(my_ready, rseq + 1, ctl);
+        if (ok && o.send_msg >= 0 && sseq + 1 > (u64)K) ok = wait_ge(my_credit, sseq + 1 - K, ctl);
+        if (ok && o.recv_msg >= 0) acquire_sys();
+        s_abort = ok ? 0 : 1;
+      }
+      __syncthreads();
+      if (s_abort) {
+        if (tid == 0) { const int pe[2] = {prev, next}; abort_peers(p, pe, 2); }
+        return;
+      }
+      if (len) {
+        const u64 coff = (u64)o.chunk * p.chunk_bytes + soff;
+        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, prev, w, rseq), len);
+        const rsrc_t out = make_rsrc(p.peer_scratch[next] + scratch_slot_off(C, K, p.slice_bytes, r, w, sseq), len);
+        const char* lsrc = p.send + coff;
+        char* ldst = p.recv + coff;
+        switch (o.kind) {
+          case kSend: move<T, OPC, VEC, kSend>(lsrc, ldst, in, out, len, tid, nt); break;
+          case kReduceSend: move<T, OPC, VEC, kReduceSend>(lsrc, ldst, in, out, len, tid, nt); break;
+          case kReduceCopySend: move<T, OPC, VEC, kReduceCopySend>(lsrc, ldst, in, out, len, tid, nt); break;
+          case kCopySend: move<T, OPC, VEC, kCopySend>(lsrc, ldst, in, out, len, tid, nt); break;
+          default: move<T, OPC, VEC, kCopy>(lsrc, ldst, in, out, len, tid, nt); break;
+        }
+      }
+      if (o.send_msg >= 0) drain_stores();
+      __syncthreads();
+      if (tid == 0) {
+        if (o.send_msg >= 0) publish(out_ready, sseq + 1, p.sys_fence);
+        if (o.recv_msg >= 0) st_sys(out_credit, rseq + 1);
+      }
+    }
+  }
+  if (tid == 0) {
+    *tx_ctr = tx_base + (u64)p.iters * mpi;
+    *rx_ctr = rx_base + (u64)p.iters * mpi;
+  }
+}
+
+// ---------------------------------------------------------------- direct kernel
+// Fold of the n-1 arriving slices of this rank's own chunk, software-pipelined by one
+// peer so two slot loads per vector are in flight; acc = op(x_q, acc) in ring order.
+// rx0[q]: sequence number of q's raw message for this slice; tx1[d]: of my result message to d
+template <typename T, int OPC, bool VEC>
+__device__ __forceinline__ void fold_and_push(const CollParams& p, const char* lsrc, char* ldst, const u64* rx0,
+                                              const u64* tx1, uint32_t nbytes, int w, int tid, int nt) {
+  const int n = p.n, r = p.rank, C = gridDim.x, K = p.nslots;
+  if (VEC) {
+    constexpr int U = 2;
+    const uint32_t nvec = nbytes >> 4;
+    for (uint32_t b = 0; b < nvec; b += (uint32_t)nt * U) {
+      v4u acc[U], cur[U], nxt[U];
+      bool live[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = b + (uint32_t)(u * nt + tid);
+        live[u] = i < nvec;
+        if (live[u]) acc[u] = ld_g16(lsrc + (size_t)i * 16);
+      }
+      {
+        const int q = direct_peer(n, r, 1);
+        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q]), nbytes);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (live[u]) cur[u] = ld_slot16(in, (b + (uint32_t)(u * nt + tid)) * 16);
+      }
+      for (int k = 1; k < n; ++k) {
+        if (k + 1 < n) {
+          const int q = direct_peer(n, r, k + 1);
+          const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q]), nbytes);
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (live[u]) nxt[u] = ld_slot16(in, (b + (uint32_t)(u * nt + tid)) * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (live[u]) acc[u] = reduce16<T, OPC>(cur[u], acc[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (live[u]) st_g16(ldst + (size_t)(b + (uint32_t)(u * nt + tid)) * 16, acc[u]);
+      for (int k = 1; k < n; ++k) {
+        const int d = direct_peer(n, r, k);
+        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slice_bytes, r, w, tx1[d]), nbytes);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (live[u]) st_slot16(out, (b + (uint32_t)(u * nt + tid)) * 16, acc[u]);
+      }
+    }
+  } else {
+    typedef typename Scal<sizeof(T)>::U Us;
+    const uint32_t ne = nbytes / sizeof(T);
+    for (uint32_t i = tid; i < ne; i += nt) {
+      T acc = reinterpret_cast<const T*>(lsrc)[i];
+      for (int k = 1; k < n; ++k) {
+        const int q = direct_peer(n, r, k);
+        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q]), nbytes);
+        const T x = __builtin_bit_cast(T, Scal<sizeof(T)>::ld(in, i * (uint32_t)sizeof(T)));
+        acc = Op<T, OPC>::f(x, acc);
+      }
+      reinterpret_cast<T*>(ldst)[i] = acc;
+      for (int k = 1; k < n; ++k) {
+        const int d = direct_peer(n, r, k);
+        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slice_bytes, r, w, tx1[d]), nbytes);
+        Scal<sizeof(T)>::st(out, i * (uint32_t)sizeof(T), __builtin_bit_cast(Us, acc));
+      }
+    }
+  }
+}
+
+template <typename T, int OPC, bool VEC>
+__global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
+  const int w = blockIdx.x, C = gridDim.x, tid = threadIdx.x, nt = blockDim.x;
+  const int n = p.n, r = p.rank, K = p.nslots;
+  __shared__ int s_abort;
+  __shared__ int s_peers[kMaxRanks];
+  // per-pair FIFO counters at the start of the call; per iteration: raw (+0), result (+1)
+  __shared__ u64 s_tx[kMaxRanks], s_rx[kMaxRanks];
+  __shared__ u64 s_rx0[kMaxRanks], s_tx1[kMaxRanks];
+  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks};
+  const int mpi = direct_msgs_per_iter();
+  if (tid < n - 1) s_peers[tid] = direct_peer(n, r, tid + 1);
+  if (tid < n) {
+    s_tx[tid] = p.tx_seq[(u64)tid * C + w];
+    s_rx[tid] = p.rx_seq[(u64)tid * C + w];
+  }
+  __syncthreads();
+
+  for (uint32_t it = 0; it < p.iters; ++it) {
+    const u64 s = (u64)it * C + w;
+    const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
+    const u64 soff = s * p.slice_bytes;
+    const u64 itoff = (u64)it * mpi;
+    if (tid < n) {
+      s_rx0[tid] = s_rx[tid] + itoff;
+      s_tx1[tid] = s_tx[tid] + itoff + 1;
+    }
+
+    // Phase A: push my raw slice of chunk d to rank d, for every peer d
+    for (int k = 1; k < n; ++k) {
+      const int d = direct_peer(n, r, k);
+      const u64 seq0 = s_tx[d] + itoff;
+      if (tid == 0) {
+        bool ok = true;
+        if (seq0 + 1 > (u64)K) ok = wait_ge(p.mbox + mbox_credit(n, C, d, w), seq0 + 1 - K, ctl);
+        s_abort = ok ? 0 : 1;
+      }
+      __syncthreads();
+      if (s_abort) goto aborted;
+      if (len) {
+        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slice_bytes, r, w, seq0), len);
+        const u64 coff = (u64)d * p.chunk_bytes + soff;
+        move<T, OPC, VEC, kSend>(p.send + coff, nullptr, out, out, len, tid, nt);
+      }
+      drain_stores();
+      __syncthreads();
+      if (tid == 0) publish(p.peer_mbox[d] + mbox_ready(C, r, w), seq0 + 1, p.sys_fence);
+    }
+
+    // Phase B: wait for the n-1 raw slices of my chunk and for slot credits of the
+    // result message at every peer; fold; store; push the result everywhere.
+    if (tid == 0) {
+      bool ok = true;
+      for (int k = 1; k < n && ok; ++k) {
+        const int q = direct_peer(n, r, k);
+        ok = wait_ge(p.mbox + mbox_ready(C, q, w), s_rx0[q] + 1, ctl);
+        if (ok && s_tx1[q] + 1 > (u64)K) ok = wait_ge(p.mbox + mbox_credit(n, C, q, w), s_tx1[q] + 1 - K, ctl);
+      }
+      if (ok) acquire_sys();
+      s_abort = ok ? 0 : 1;
+    }
+    __syncthreads();
+    if (s_abort) goto aborted;
+    if (len) {
+      const u64 coff = (u64)r * p.chunk_bytes + soff;
+      fold_and_push<T, OPC, VEC>(p, p.send + coff, p.recv + coff, s_rx0, s_tx1, len, w, tid, nt);
+    }
+    drain_stores();
+    __syncthreads();
+    if (tid == 0) {
+      for (int k = 1; k < n; ++k) {
+        const int q = direct_peer(n, r, k);
+        st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), s_rx0[q] + 1);  // raw slot consumed
+      }
+      for (int k = 1; k < n; ++k) {
+        const int d = direct_peer(n, r, k);
+        publish(p.peer_mbox[d] + mbox_ready(C, r, w), s_tx1[d] + 1, p.sys_fence);
+      }
+    }
+
+    // Phase C: store every peer's result slice
+    for (int k = 1; k < n; ++k) {
+      const int q = direct_peer(n, r, k);
+      const u64 seq1 = s_rx0[q] + 1;
+      if (tid == 0) {
+        const bool ok = wait_ge(p.mbox + mbox_ready(C, q, w), seq1 + 1, ctl);
+        if (ok) acquire_sys();
+        s_abort = ok ? 0 : 1;
+      }
+      __syncthreads();
+      if (s_abort) goto aborted;
+      if (len) {
+        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, seq1), len);
+        const u64 coff = (u64)q * p.chunk_bytes + soff;
+        move<T, OPC, VEC, kCopy>(nullptr, p.recv + coff, in, in, len, tid, nt);
+      }
+      __syncthreads();
+      if (tid == 0) st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), seq1 + 1);
+    }
+  }
+  if (tid < n && tid != r) {
+    p.tx_seq[(u64)tid * C + w] = s_tx[tid] + (u64)p.iters * mpi;
+    p.rx_seq[(u64)tid * C + w] = s_rx[tid] + (u64)p.iters * mpi;
+  }
+  return;
+aborted:
+  if (tid == 0) abort_peers(p, s_peers, n - 1);
+}
+
+// ---------------------------------------------------------------- local reduce
+template <typename T, int OPC>
+__global__ void __launch_bounds__(256) local_reduce_vec(char* __restrict__ out, const char* __restrict__ a,
+                                                        const char* __restrict__ b, u64 nvec) {
+  constexpr int U = 4;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 base = (u64)blockIdx.x * blockDim.x * U + threadIdx.x; base < nvec; base += stride * U) {
+    v4u x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const u64 i = base + (u64)u * blockDim.x;
+      if (i < nvec) {
+        x[u] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(a) + i);
+        y[u] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(b) + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const u64 i = base + (u64)u * blockDim.x;
+      if (i < nvec) __builtin_nontemporal_store(reduce16<T, OPC>(x[u], y[u]), reinterpret_cast<v4u*>(out) + i);
+    }
+  }
+}
+
+template <typename T, int OPC>
+__global__ void __launch_bounds__(256) local_reduce_scalar(T* __restrict__ out, const T* __restrict__ a,
+                                                           const T* __restrict__ b, u64 n) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = Op<T, OPC>::f(a[i], b[i]);
+}
+
+// ---------------------------------------------------------------- dispatch
+template <template <typename, int, bool> class K>
+struct Unused {};
+
+#define MNCCL_DISPATCH_T(dtype, MACRO)      \
+  switch (dtype) {                          \
+    case kF32: MACRO(float); break;         \
+    case kF64: MACRO(double); break;        \
+    case kI32: MACRO(int32_t); break;       \
+    case kF16: MACRO(_Float16); break;      \
+    case kBF16: MACRO(bf16_t); break;       \
+    default: return hipErrorInvalidValue;   \
+  }
+
+template <typename T>
+static hipError_t ring_for_t(int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
+#define RING_CASE(OPC)                                                                           \
+  case OPC:                                                                                      \
+    if (vec) hipLaunchKernelGGL((ring_kernel<T, OPC, true>), dim3(C), dim3(nt), 0, st, p);      \
+    else hipLaunchKernelGGL((ring_kernel<T, OPC, false>), dim3(C), dim3(nt), 0, st, p);         \
+    break;
+  switch (op) {
+    RING_CASE(kSum) RING_CASE(kProd) RING_CASE(kMax) RING_CASE(kMin)
+    default: return hipErrorInvalidValue;
+  }
+#undef RING_CASE
+  return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t direct_for_t(int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
+#define DIRECT_CASE(OPC)                                                                         \
+  case OPC:                                                                                      \
+    if (vec) hipLaunchKernelGGL((direct_kernel<T, OPC, true>), dim3(C), dim3(nt), 0, st, p);    \
+    else hipLaunchKernelGGL((direct_kernel<T, OPC, false>), dim3(C), dim3(nt), 0, st, p);       \
+    break;
+  switch (op) {
+    DIRECT_CASE(kSum) DIRECT_CASE(kProd) DIRECT_CASE(kMax) DIRECT_CASE(kMin)
+    default: return hipErrorInvalidValue;
+  }
+#undef DIRECT_CASE
+  return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t local_for_t(int op, void* out, const void* a, const void* b, u64 count, hipStream_t st) {
+  const bool vec = (((uintptr_t)out | (uintptr_t)a | (uintptr_t)b) % 16 == 0) && ((count * sizeof(T)) % 16 == 0);
+  const u64 nvec = count * sizeof(T) / 16;
+  const int nt = 256;
+  const u64 want = vec ? (nvec + (u64)nt * 4 - 1) / ((u64)nt * 4) : (count + nt - 1) / nt;
+  const int grid = (int)(want < 4096 ? (want ? want : 1) : 4096);
+#define LOCAL_CASE(OPC)                                                                              \
+  case OPC:                                                                                          \
+    if (vec)                                                                                         \
+      hipLaunchKernelGGL((local_reduce_vec<T, OPC>), dim3(grid), dim3(nt), 0, st, (char*)out,       \
+                         (const char*)a, (const char*)b, nvec);                                      \
+    else                                                                                             \
+      hipLaunchKernelGGL((local_reduce_scalar<T, OPC>), dim3(grid), dim3(nt), 0, st, (T*)out,       \
+                         (const T*)a, (const T*)b, count);                                           \
+    break;
+  switch (op) {
+    LOCAL_CASE(kSum) LOCAL_CASE(kProd) LOCAL_CASE(kMax) LOCAL_CASE(kMin)
+    default: return hipErrorInvalidValue;
+  }
+#undef LOCAL_CASE
+  return hipGetLastError();
+}
+
+hipError_t launch_ring(int dtype, int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
+#define M(T) return ring_for_t<T>(op, vec, C, nt, p, st)
+  MNCCL_DISPATCH_T(dtype, M)
+#undef M
+}
+
+hipError_t launch_direct(int dtype, int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
+#define M(T) return direct_for_t<T>(op, vec, C, nt, p, st)
+  MNCCL_DISPATCH_T(dtype, M)
+#undef M
+}
+
+hipError_t launch_local_reduce(int dtype, int op, void* out, const void* local, const void* incoming, uint64_t count,
+                               hipStream_t st) {
+  if (count == 0) return hipSuccess;
+#define M(T) return local_for_t<T>(op, out, local, incoming, count, st)
+  MNCCL_DISPATCH_T(dtype, M)
+#undef M
+}
+
+bool dtype_supported(int dtype) { return dtype_size(dtype) != 0; }
+
+int dtype_size(int dtype) {
+  switch (dtype) {
+    case kF32: case kI32: return 4;
+    case kF64: return 8;
+    case kF16: case kBF16: return 2;
+    default: return 0;
+  }
+}
+
+}  // namespace mnccl

@@ -1,0 +1,108 @@
+// schedule.h -- the per-channel message schedules, shared verbatim by the HIP kernels
+// (kernels.hip) and by the host-side schedule simulator (sim.cpp, run by the CPU test
+// suite), so the index math the GPU executes is the index math the CPU tests check.
+//
+// Ring (reference mini_nccl.cu:108-194).  The reference walks step-major: for each step,
+// every slice of the chunk.  Each element's arithmetic depends only on which chunk it
+// is in, so we walk slice-major per channel instead (for each slice owned by the
+// channel, all 2(n-1) steps), which keeps every link busy with a 2-slot FIFO and gives
+// per element exactly the reference's sequence of ops:
+//   op 0         : send the raw chunk r                         (SR step 0 send, :128-131)
+//   op 1..n-1    : SR step i = op-1 receives chunk (r-i-1) mod n (:110) and reduces
+//                  op(local, incoming) (:126); i < n-2 forwards the partial (the next
+//                  step's send of the same chunk, :109), i == n-2 is the final value of
+//                  chunk r+1: stored to recv AND forwarded (all-gather step 0, :160)
+//   op n..2n-2   : AG step j = op-n receives chunk (r-j) mod n (:172, the sender's
+//                  send_idx (r-1)-j+1), stores it to recv, forwards unless j == n-2.
+// Messages per channel iteration: 2(n-1) sent to r+1, 2(n-1) received from r-1.
+//
+// Direct (same fold order, all links): per slice, rank r pushes its raw slice of every
+// chunk d != r to rank d, folds the n-1 arriving slices of its own chunk in ring order
+// r, r+1, ..., r-1 (acc = op(x_q, acc): the visited rank's value is the LEFT/local
+// operand exactly as at rank q of the ring), stores and pushes the result to every peer,
+// and stores the n-1 results it receives.  Messages per pair and iteration: 2.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define MNCCL_HD __host__ __device__ __forceinline__
+#else
+#define MNCCL_HD inline
+#endif
+
+namespace mnccl {
+
+enum RingKind : int {
+  kSend = 0,            // out <- local
+  kReduceSend = 1,      // out <- op(local, in)
+  kReduceCopySend = 2,  // v = op(local, in); recv <- v; out <- v
+  kCopySend = 3,        // recv <- in; out <- in
+  kCopy = 4             // recv <- in
+};
+
+struct RingOp {
+  int kind;
+  int chunk;     // chunk index the op touches
+  int send_msg;  // message index (within the iteration) sent to r+1, or -1
+  int recv_msg;  // message index received from r-1, or -1
+};
+
+MNCCL_HD int mod_n(int a, int n) { return ((a % n) + n) % n; }
+
+MNCCL_HD int ring_num_ops(int n) { return 2 * n - 1; }
+MNCCL_HD int ring_msgs_per_iter(int n) { return 2 * (n - 1); }
+
+MNCCL_HD RingOp ring_op(int n, int r, int k) {
+  RingOp o;
+  if (k == 0) {
+    o.kind = kSend; o.chunk = r; o.send_msg = 0; o.recv_msg = -1;
+  } else if (k < n) {
+    const int i = k - 1;
+    o.kind = (i < n - 2) ? kReduceSend : kReduceCopySend;
+    o.chunk = mod_n(r - i - 1, n);
+    o.send_msg = k; o.recv_msg = k - 1;
+  } else {
+    const int j = k - n;
+    o.kind = (j < n - 2) ? kCopySend : kCopy;
+    o.chunk = mod_n(r - j, n);
+    o.send_msg = (j < n - 2) ? k : -1;
+    o.recv_msg = k - 1;
+  }
+  return o;
+}
+
+// Direct schedule: peer order for pushes and for the fold.
+MNCCL_HD int direct_peer(int n, int r, int k) { return mod_n(r + k, n); }  // k = 1..n-1
+MNCCL_HD int direct_msgs_per_iter() { return 2; }  // per (pair, channel): raw, then final
+
+// Slice geometry shared by both schedules: channel w owns slices w, w+C, w+2C, ...
+// of every chunk; message bytes of slice s (0 for the padding slices past the end, which
+// still move flags so every channel sends the same number of messages).
+MNCCL_HD uint64_t slice_len(uint64_t chunk_bytes, uint64_t slice_bytes, uint64_t s) {
+  const uint64_t off = s * slice_bytes;
+  if (off >= chunk_bytes) return 0;
+  const uint64_t rest = chunk_bytes - off;
+  return rest < slice_bytes ? rest : slice_bytes;
+}
+
+// Mailbox layout (uint64 words, one 128-byte line per flag):
+//   READY(src, w)  : written by rank src when its message for this rank landed
+//   CREDIT(dst, w) : written by rank dst when it has consumed a message from this rank
+//   ABORT          : written by any rank that gives up (timeout / host abort)
+constexpr int kFlagStride = 16;  // uint64 words per flag line
+MNCCL_HD uint64_t mbox_ready(int C, int src, int w) { return ((uint64_t)src * C + w) * kFlagStride; }
+MNCCL_HD uint64_t mbox_credit(int n, int C, int dst, int w) { return ((uint64_t)n * C + (uint64_t)dst * C + w) * kFlagStride; }
+MNCCL_HD uint64_t mbox_abort(int n, int C) { return (uint64_t)2 * n * C * kFlagStride; }
+MNCCL_HD uint64_t mbox_words(int n, int C) { return mbox_abort(n, C) + kFlagStride; }
+
+// Scratch layout: region per source rank, [C][slots][slice_bytes] each.
+MNCCL_HD uint64_t scratch_region_bytes(int C, int slots, uint64_t slice_bytes) { return (uint64_t)C * slots * slice_bytes; }
+MNCCL_HD uint64_t scratch_slot_off(int C, int slots, uint64_t slice_bytes, int src, int w, uint64_t seq) {
+  return (uint64_t)src * scratch_region_bytes(C, slots, slice_bytes) +
+         ((uint64_t)w * slots + (seq % (uint64_t)slots)) * slice_bytes;
+}
+
+// Kernel status bits (host-mapped status word)
+enum : uint32_t { kStatusTimeout = 1u, kStatusHostAbort = 2u, kStatusRemoteAbort = 4u };
+
+}  // namespace mnccl

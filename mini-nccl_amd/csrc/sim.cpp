@@ -1,0 +1,301 @@
+// sim.cpp -- host-side simulator of the ring / direct kernels' protocol, for the CPU test
+// suite (no GPU).  Each (rank, channel) runs the same op sequence as kernels.hip, using the
+// same schedule.h index math, scratch layout and mailbox layout; a wait that is not
+// satisfied yields, and the scheduler round-robins over all programs.  It checks:
+//   * the data each rank ends with (compared by the tests against oracle/ring_oracle.c),
+//   * deadlock freedom for the given (n, channels, slots, sizes): no progress => -1,
+//   * that the per-channel sequence bases carried across calls keep flags consistent.
+// fp32 only (the schedule does not depend on the element type); ops as reference
+// mini_nccl.cu:38-41 with a = local, b = incoming.
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "schedule.h"
+
+using namespace mnccl;
+
+namespace {
+
+float apply(int op, float a, float b) {
+  switch (op) {
+    case 0: return a + b;
+    case 1: return a * b;
+    case 2: return (a > b) ? a : b;
+    default: return (a < b) ? a : b;
+  }
+}
+
+struct World {
+  int n, C, K, op, algo;
+  uint64_t slice, chunk_bytes, nslices;
+  uint32_t iters;
+  std::vector<const float*> send;
+  std::vector<float*> recv;
+  std::vector<std::vector<char>> scratch;     // per rank
+  std::vector<std::vector<uint64_t>> mbox;    // per rank
+  std::vector<std::vector<uint64_t>> tx_seq, rx_seq;  // per rank: [peer * C + w]
+
+  char* slot(int owner, int src, int w, uint64_t seq) {
+    return scratch[owner].data() + scratch_slot_off(C, K, slice, src, w, seq);
+  }
+  uint64_t& ready(int owner, int src, int w) { return mbox[owner][mbox_ready(C, src, w)]; }
+  uint64_t& credit(int owner, int dst, int w) { return mbox[owner][mbox_credit(n, C, dst, w)]; }
+};
+
+// copy / reduce over `bytes` bytes of floats
+void do_move(int kind, int op, const float* local, const float* in, float* recv, float* out, uint64_t bytes) {
+  const uint64_t ne = bytes / 4;
+  for (uint64_t i = 0; i < ne; ++i) {
+    float v;
+    switch (kind) {
+      case kSend: v = local[i]; break;
+      case kReduceSend:
+      case kReduceCopySend: v = apply(op, local[i], in[i]); break;
+      default: v = in[i]; break;
+    }
+    if (kind == kReduceCopySend || kind == kCopySend || kind == kCopy) recv[i] = v;
+    if (kind != kCopy) out[i] = v;
+  }
+}
+
+struct Prog {
+  int r, w;
+  uint32_t it = 0;
+  int k = 0;  // op index within the iteration
+  bool done = false;
+};
+
+// One ring op (kernels.hip ring_kernel body); returns false if a wait is unsatisfied.
+bool ring_step(World& W, Prog& P) {
+  const int n = W.n, r = P.r, w = P.w, K = W.K;
+  const int prev = mod_n(r - 1, n), next = mod_n(r + 1, n);
+  const uint64_t tx_base = W.tx_seq[r][(size_t)next * W.C + w], rx_base = W.rx_seq[r][(size_t)prev * W.C + w];
+  const int mpi = ring_msgs_per_iter(n);
+  const uint64_t s = (uint64_t)P.it * W.C + w;
+  const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
+  const uint64_t soff = s * W.slice;
+  const uint64_t itoff = (uint64_t)P.it * mpi;
+  const RingOp o = ring_op(n, r, P.k);
+  const uint64_t rseq = rx_base + itoff + (uint64_t)o.recv_msg, sseq = tx_base + itoff + (uint64_t)o.send_msg;
+  if (o.recv_msg >= 0 && W.ready(r, prev, w) < rseq + 1) return false;
+  if (o.send_msg >= 0 && sseq + 1 > (uint64_t)K && W.credit(r, next, w) < sseq + 1 - K) return false;
+  if (len) {
+    const uint64_t coff = (uint64_t)o.chunk * W.chunk_bytes + soff;
+    const float* local = (const float*)((const char*)W.send[r] + coff);
+    float* recv = (float*)((char*)W.recv[r] + coff);
+    const float* in = o.recv_msg >= 0 ? (const float*)W.slot(r, prev, w, rseq) : nullptr;
+    float* out = o.send_msg >= 0 ? (float*)W.slot(next, r, w, sseq) : nullptr;
+    do_move(o.kind, W.op, local, in, recv, out, len);
+  }
+  if (o.send_msg >= 0) W.ready(next, r, w) = sseq + 1;
+  if (o.recv_msg >= 0) W.credit(prev, r, w) = rseq + 1;
+  if (++P.k == ring_num_ops(n)) {
+    P.k = 0;
+    if (++P.it == W.iters) P.done = true;
+  }
+  return true;
+}
+
+// One direct op (kernels.hip direct_kernel): k in [0, n-1) phase A, k == n-1 phase B,
+// k in [n, 2n-1) phase C.
+bool direct_step(World& W, Prog& P) {
+  const int n = W.n, r = P.r, w = P.w, K = W.K;
+  const uint64_t s = (uint64_t)P.it * W.C + w;
+  const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
+  const uint64_t soff = s * W.slice;
+  const uint64_t itoff = (uint64_t)P.it * direct_msgs_per_iter();
+  // per-pair FIFO positions: raw message of this iteration = +0, result = +1
+  auto tx0 = [&](int d) { return W.tx_seq[r][(size_t)d * W.C + w] + itoff; };
+  auto rx0 = [&](int q) { return W.rx_seq[r][(size_t)q * W.C + w] + itoff; };
+  if (P.k < n - 1) {
+    const int d = direct_peer(n, r, P.k + 1);
+    const uint64_t seq0 = tx0(d);
+    if (seq0 + 1 > (uint64_t)K && W.credit(r, d, w) < seq0 + 1 - K) return false;
+    if (len) {
+      const uint64_t coff = (uint64_t)d * W.chunk_bytes + soff;
+      do_move(kSend, W.op, (const float*)((const char*)W.send[r] + coff), nullptr, nullptr, (float*)W.slot(d, r, w, seq0),
+              len);
+    }
+    W.ready(d, r, w) = seq0 + 1;
+  } else if (P.k == n - 1) {
+    for (int k = 1; k < n; ++k) {
+      const int q = direct_peer(n, r, k);
+      if (W.ready(r, q, w) < rx0(q) + 1) return false;
+      if (tx0(q) + 2 > (uint64_t)K && W.credit(r, q, w) < tx0(q) + 2 - K) return false;
+    }
+    if (len) {
+      const uint64_t coff = (uint64_t)r * W.chunk_bytes + soff;
+      const float* local = (const float*)((const char*)W.send[r] + coff);
+      float* recv = (float*)((char*)W.recv[r] + coff);
+      for (uint64_t i = 0; i < len / 4; ++i) {
+        float acc = local[i];
+        for (int k = 1; k < n; ++k) {
+          const int q = direct_peer(n, r, k);
+          acc = apply(W.op, ((const float*)W.slot(r, q, w, rx0(q)))[i], acc);
+        }
+        recv[i] = acc;
+        for (int k = 1; k < n; ++k) {
+          const int d = direct_peer(n, r, k);
+          ((float*)W.slot(d, r, w, tx0(d) + 1))[i] = acc;
+        }
+      }
+    }
+    for (int k = 1; k < n; ++k) W.credit(direct_peer(n, r, k), r, w) = rx0(direct_peer(n, r, k)) + 1;
+    for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx0(direct_peer(n, r, k)) + 2;
+  } else {
+    const int q = direct_peer(n, r, P.k - n + 1);
+    const uint64_t seq1 = rx0(q) + 1;
+    if (W.ready(r, q, w) < seq1 + 1) return false;
+    if (len) {
+      const uint64_t coff = (uint64_t)q * W.chunk_bytes + soff;
+      do_move(kCopy, W.op, nullptr, (const float*)W.slot(r, q, w, seq1), (float*)((char*)W.recv[r] + coff), nullptr, len);
+    }
+    W.credit(q, r, w) = seq1 + 1;
+  }
+  if (++P.k == 2 * n - 1) {
+    P.k = 0;
+    if (++P.it == W.iters) P.done = true;
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Runs `calls` consecutive all-reduces (send -> recv, fp32) on n simulated ranks with the
+// GPU kernels' protocol; call i uses schedule (algo >> i) & 1 (so schedules can alternate
+// on one communicator state, as mncclCommSetAlgo allows).  schedule_seed != 0 permutes the order programs are tried in
+// (pseudo-random), exploring different interleavings.  Returns 0, -1 on deadlock,
+// -2 on bad arguments.  *steps_out = ops executed.
+int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, int n, uint64_t count, int op,
+                        uint64_t slice_bytes, int channels, int slots, int calls, uint64_t schedule_seed,
+                        uint64_t* steps_out) {
+  if (n < 1 || n > 16 || channels < 1 || slots < 1 || slice_bytes < 4 || slice_bytes % 4) return -2;
+  World W;
+  W.n = n; W.C = channels; W.K = slots; W.op = op; W.algo = algo; W.slice = slice_bytes;
+  const uint64_t chunk = count / (uint64_t)n;
+  W.chunk_bytes = chunk * 4;
+  W.nslices = (W.chunk_bytes + slice_bytes - 1) / slice_bytes;
+  W.iters = (uint32_t)((W.nslices + (uint64_t)channels - 1) / (uint64_t)channels);
+  W.send.assign(send, send + n);
+  W.recv.assign(recv, recv + n);
+  W.scratch.assign((size_t)n, std::vector<char>((size_t)n * scratch_region_bytes(channels, slots, slice_bytes)));
+  W.mbox.assign((size_t)n, std::vector<uint64_t>((size_t)mbox_words(n, channels), 0));
+  W.tx_seq.assign((size_t)n, std::vector<uint64_t>((size_t)n * channels, 0));
+  W.rx_seq.assign((size_t)n, std::vector<uint64_t>((size_t)n * channels, 0));
+  uint64_t steps = 0;
+  uint64_t rng = schedule_seed * 6364136223846793005ull + 1442695040888963407ull;
+  for (int call = 0; call < calls; ++call) {
+    const int a = (algo >> call) & 1;
+    for (int r = 0; r < n; ++r) {  // send -> recv copy of the tail (Comm::allreduce)
+      const uint64_t body = W.chunk_bytes * (uint64_t)n;
+      if (n == 1 || chunk == 0) memcpy(recv[r], send[r], count * 4);
+      else if (count * 4 > body) memcpy((char*)recv[r] + body, (const char*)send[r] + body, count * 4 - body);
+    }
+    if (n == 1 || chunk == 0) continue;
+    std::vector<Prog> progs;
+    for (int r = 0; r < n; ++r)
+      for (int w = 0; w < channels; ++w) {
+        Prog p;
+        p.r = r; p.w = w;
+        p.done = W.iters == 0;
+        progs.push_back(p);
+      }
+    for (;;) {
+      bool any = false, all_done = true;
+      const size_t np = progs.size();
+      const size_t start = schedule_seed ? (size_t)((rng >> 33) % np) : 0;
+      for (size_t j = 0; j < np; ++j) {
+        Prog& P = progs[(start + j) % np];
+        if (P.done) continue;
+        all_done = false;
+        // a random number of ops per turn for this program when seeded
+        int burst = 1;
+        if (schedule_seed) {
+          rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+          burst = 1 + (int)((rng >> 40) % 4);
+        }
+        for (int b = 0; b < burst && !P.done; ++b) {
+          const bool ok = a == 1 ? direct_step(W, P) : ring_step(W, P);
+          if (!ok) break;
+          any = true;
+          ++steps;
+        }
+      }
+      if (schedule_seed) rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+      if (all_done) break;
+      if (!any) return -1;  // deadlock
+    }
+    // the kernels' last action per channel: advance the per-pair FIFO counters
+    for (int r = 0; r < n; ++r)
+      for (int w = 0; w < channels; ++w) {
+        if (a == 1) {
+          for (int q = 0; q < n; ++q) {
+            if (q == r) continue;
+            W.tx_seq[r][(size_t)q * channels + w] += (uint64_t)W.iters * direct_msgs_per_iter();
+            W.rx_seq[r][(size_t)q * channels + w] += (uint64_t)W.iters * direct_msgs_per_iter();
+          }
+        } else {
+          const uint64_t m = (uint64_t)W.iters * ring_msgs_per_iter(n);
+          W.tx_seq[r][(size_t)mod_n(r + 1, n) * channels + w] += m;
+          W.rx_seq[r][(size_t)mod_n(r - 1, n) * channels + w] += m;
+        }
+      }
+  }
+  if (steps_out) *steps_out = steps;
+  return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// Host-only hooks for the CPU test suite: the bootstrap (TCP star) and the env config,
+// exercised without a GPU.  Not part of libmini_nccl.so.
+#include <stdio.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "bootstrap.h"
+#include "config.h"
+
+extern "C" {
+
+// connect, all-gather a 256-byte record per rank, barrier twice; 0 on success,
+// -1 on exception, -2 if gathered contents are wrong.
+int mnccl_bootstrap_selftest(int rank, int nranks, const char* ip, int port, int timeout_ms) {
+  try {
+    mnccl::Bootstrap b;
+    b.connect(rank, nranks, ip ? ip : "127.0.0.1", port, timeout_ms / 1000.0);
+    unsigned char mine[256];
+    for (int i = 0; i < 256; ++i) mine[i] = (unsigned char)(rank * 31 + i);
+    std::vector<unsigned char> all((size_t)nranks * 256);
+    b.allgather(mine, all.data(), 256);
+    b.barrier();
+    for (int r = 0; r < nranks; ++r)
+      for (int i = 0; i < 256; ++i)
+        if (all[(size_t)r * 256 + i] != (unsigned char)(r * 31 + i)) return -2;
+    b.barrier();
+    return 0;
+  } catch (const std::exception& e) {
+    fprintf(stderr, "bootstrap selftest rank %d: %s\n", rank, e.what());
+    return -1;
+  }
+}
+
+// Config::from_env() rendered to text; -1 if the environment is invalid.
+int mnccl_config_describe(char* buf, int len) {
+  try {
+    const std::string s = mnccl::Config::from_env().describe();
+    snprintf(buf, (size_t)len, "%s", s.c_str());
+    return 0;
+  } catch (const std::exception& e) {
+    snprintf(buf, (size_t)len, "%s", e.what());
+    return -1;
+  }
+}
+
+}  // extern "C"

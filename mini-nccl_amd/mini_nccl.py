@@ -1,0 +1,151 @@
+"""ctypes binding of libmini_nccl.so -- the host-side mirror of the reference's C ABI.
+
+The reference's callers are C++ programs linking ``libmini_nccl.so``
+(``tests/perf_test.cpp``, ``src/main.cpp``); ``apps/`` holds the C++ equivalents.
+This module exposes the same six entry points (``include/mini_nccl_api.h``) plus the
+extensions of ``include/mini_nccl_ext.h`` to Python for the test suite and
+``bench.py``.  Names, argument meaning and return codes are the C ones: every
+function returns an ``ncclResult_t`` integer, exactly as the C ABI does.
+
+Device memory and streams are passed as raw integers (device pointers / hipStream_t),
+so any allocator works: torch tensors (``t.data_ptr()``, ``torch.cuda.Stream().cuda_stream``)
+or the raw HIP runtime (``tests/hip_rt.py``).  There is no CPU fallback: if the
+library is missing, :func:`load` raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libmini_nccl.so")
+
+# ncclResult_t (include/mini_nccl_api.h; reference include/mini_nccl_api.h:15-24)
+ncclSuccess = 0
+ncclUnhandledCudaError = 1
+ncclSystemError = 2
+ncclInternalError = 3
+ncclInvalidArgument = 4
+ncclInvalidUsage = 5
+ncclRemoteError = 6
+ncclInProgress = 7
+
+# ncclDataType_t (reference :29-40)
+ncclInt8, ncclUint8, ncclInt32, ncclUint32, ncclInt64, ncclUint64 = 0, 1, 2, 3, 4, 5
+ncclFloat16, ncclFloat, ncclDouble, ncclBfloat16 = 6, 7, 8, 9
+
+# ncclRedOp_t (reference :43-49)
+ncclSum, ncclProd, ncclMax, ncclMin, ncclAvg = 0, 1, 2, 3, 4
+
+# mncclAlgo_t
+ALGO_RING, ALGO_DIRECT = 0, 1
+
+DTYPE_SIZE = {ncclInt32: 4, ncclFloat16: 2, ncclFloat: 4, ncclDouble: 8, ncclBfloat16: 2}
+
+
+class CommInfo(ctypes.Structure):
+    _fields_ = [
+        ("rank", ctypes.c_int), ("nranks", ctypes.c_int), ("device", ctypes.c_int),
+        ("slice_bytes", ctypes.c_size_t), ("window", ctypes.c_int), ("signal_batch", ctypes.c_int),
+        ("channels", ctypes.c_int), ("slots", ctypes.c_int), ("threads", ctypes.c_int),
+        ("algo", ctypes.c_int), ("blocking", ctypes.c_int), ("sys_fence", ctypes.c_int),
+        ("timeout_s", ctypes.c_double), ("scratch_bytes", ctypes.c_size_t),
+    ]
+
+
+# every entry point of include/mini_nccl_api.h and include/mini_nccl_ext.h: (restype, argtypes)
+_VP, _SZ, _I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+SIGNATURES = {
+    "ncclGetErrorString": (ctypes.c_char_p, [_I]),
+    "ncclCommInitRank": (_I, [ctypes.POINTER(_VP), _I, _I, ctypes.c_char_p]),
+    "ncclCommDestroy": (_I, [_VP]),
+    "ncclCommUserRank": (_I, [_VP, ctypes.POINTER(_I)]),
+    "ncclCommCount": (_I, [_VP, ctypes.POINTER(_I)]),
+    "ncclAllReduce": (_I, [_VP, _VP, _SZ, _I, _I, _VP, _VP]),
+    "mncclLocalReduce": (_I, [_VP, _VP, _VP, _SZ, _I, _I, _VP]),
+    "mncclCommGetAsyncError": (_I, [_VP, ctypes.POINTER(_I)]),
+    "mncclCommGetInfo": (_I, [_VP, ctypes.POINTER(CommInfo)]),
+    "mncclCommSetAlgo": (_I, [_VP, _I]),
+    "mncclVersion": (_I, []),
+}
+
+_lib = None
+
+
+def load(path=None):
+    """Load libmini_nccl.so (raises OSError if it is missing: no fallback)."""
+    global _lib
+    if _lib is None or path is not None:
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise OSError(f"{p} not built: run `make -C mini-nccl_amd` (or __graft_entry__.build())")
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def get_error_string(result):
+    return load().ncclGetErrorString(int(result)).decode()
+
+
+class NcclError(RuntimeError):
+    def __init__(self, code, what=""):
+        super().__init__(f"{what}: {get_error_string(code)} ({code})")
+        self.code = code
+
+
+def check(code, what="mini-nccl"):
+    if code != ncclSuccess:
+        raise NcclError(code, what)
+    return code
+
+
+class Comm:
+    """Thin RAII wrapper over ncclComm_t (the calls themselves are the C functions)."""
+
+    def __init__(self, nranks, rank, ip="127.0.0.1"):
+        lib = load()
+        self.handle = ctypes.c_void_p()
+        check(lib.ncclCommInitRank(ctypes.byref(self.handle), nranks, rank, ip.encode() if ip else None),
+              "ncclCommInitRank")
+
+    def all_reduce(self, send_ptr, recv_ptr, count, dtype=ncclFloat, op=ncclSum, stream=0):
+        """Returns the ncclResult_t (does not raise) -- the reference's calling convention."""
+        return load().ncclAllReduce(send_ptr, recv_ptr, count, dtype, op, self.handle, stream)
+
+    def rank(self):
+        r = ctypes.c_int()
+        check(load().ncclCommUserRank(self.handle, ctypes.byref(r)))
+        return r.value
+
+    def count(self):
+        c = ctypes.c_int()
+        check(load().ncclCommCount(self.handle, ctypes.byref(c)))
+        return c.value
+
+    def info(self):
+        i = CommInfo()
+        check(load().mncclCommGetInfo(self.handle, ctypes.byref(i)))
+        return {f: getattr(i, f) for f, _ in CommInfo._fields_}
+
+    def set_algo(self, algo):
+        return check(load().mncclCommSetAlgo(self.handle, algo))
+
+    def async_error(self):
+        e = ctypes.c_int()
+        check(load().mncclCommGetAsyncError(self.handle, ctypes.byref(e)))
+        return e.value
+
+    def destroy(self):
+        if self.handle:
+            code = load().ncclCommDestroy(self.handle)
+            self.handle = ctypes.c_void_p()
+            return code
+        return ncclSuccess
+
+
+def local_reduce(out_ptr, local_ptr, incoming_ptr, count, dtype=ncclFloat, op=ncclSum, stream=0):
+    """out[i] = op(local[i], incoming[i]) on the GPU (the scatter-reduce element-wise kernel)."""
+    return load().mncclLocalReduce(out_ptr, local_ptr, incoming_ptr, count, dtype, op, stream)

@@ -1,0 +1,163 @@
+"""Rank processes for the multi-process GPU tests (spawned; one process = one rank).
+
+The reference tests several ranks sharing GPU 0 (tests/perf_test.cpp:46); the 1-GPU
+test box does the same: every rank opens the others' scratch/mailbox through HIP IPC
+on the same device, so the whole cross-process protocol (bootstrap, IPC mapping,
+flags, credits, sequence continuation, aborts) runs for real.  The oracle each rank
+compares against is computed in-process from the same seeded inputs.
+"""
+import os
+import sys
+import time
+import traceback
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (HERE, os.path.join(ROOT, "mini-nccl_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint8)
+
+
+def compare(got, exp, dtype, arith):
+    """Number of mismatching elements: bit-exact, except NaN payloads of arithmetic ops."""
+    if dtype in ("f32", "f64", "f16") and arith:
+        gn, en = np.isnan(got), np.isnan(exp)
+        bad = (gn != en) | (~gn & (got.view(np.uint8).reshape(got.size, -1) != exp.view(np.uint8).reshape(exp.size, -1)).any(axis=1))
+        return int(bad.sum()), (int(np.argmax(bad)) if bad.any() else -1)
+    eq = (got.view(np.uint8).reshape(got.size, -1) == exp.view(np.uint8).reshape(exp.size, -1)).all(axis=1)
+    return int((~eq).sum()), (int(np.argmin(eq)) if not eq.all() else -1)
+
+
+def make_inputs(n, count, dtype, seed, special):
+    import oracle_api as O
+    xs = O.random_inputs(n, count, dtype, seed=seed)
+    if special and dtype in ("f32", "f64"):
+        vals = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-40, -1e-40], dtype=xs[0].dtype)
+        for r, x in enumerate(xs):
+            g = np.random.default_rng(seed * 31 + r)
+            k = g.choice(count, size=min(count, 64), replace=False)
+            x[k] = vals[np.arange(k.size) % vals.size]
+    return xs
+
+
+def allreduce_rank(rank, n, port, cases, env, out_q):
+    """Run `cases` on one communicator; report per-case mismatch counts."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        hip_rt.set_device(int(env.get("TEST_DEVICE", "0")))
+        comm = M.Comm(n, rank, "127.0.0.1")
+        stream = hip_rt.Stream()
+        results = []
+        for case in cases:
+            dtype, op, count, inplace, algo, calls, seed = (case[k] for k in
+                                                            ("dtype", "op", "count", "inplace", "algo", "calls", "seed"))
+            comm.set_algo(algo)
+            if case.get("known") == "ones":  # perf_test.cpp:81-84
+                xs = [np.ones(count, dtype=np.float32) for _ in range(n)]
+            else:
+                xs = make_inputs(n, count, dtype, seed, case.get("special", False))
+            exp = O.allreduce(xs, dtype, op, inplace=inplace)[rank]
+            code, npd = O.DTYPES[dtype]
+            nbytes = xs[rank].nbytes
+            off = case.get("offset", 0)  # misaligned base (bytes) -> scalar path
+            send = hip_rt.DeviceBuffer(nbytes + off)
+            recv = send if inplace else hip_rt.DeviceBuffer(nbytes + off)
+            if not inplace:
+                recv.fill_byte(0xAB)
+            rc = 0
+            t0 = time.time()
+            for c in range(calls):
+                send.upload(xs[rank], off)
+                rc = comm.all_reduce(send.ptr + off, recv.ptr + off, count, code, O.OPS[op], stream.handle)
+                if rc != 0:
+                    break
+            stream.sync()
+            dt = time.time() - t0
+            got = recv.download(npd, count, off)
+            bad, first = compare(got, exp, dtype, op in ("sum", "prod")) if rc == 0 else (-1, -1)
+            results.append({"case": case, "rc": rc, "bad": bad, "first": first, "secs": dt,
+                            "async": comm.async_error()})
+            send.free()
+            if not inplace:
+                recv.free()
+        stream.destroy()
+        info = comm.info()
+        rc = comm.destroy()
+        out_q.put((rank, {"results": results, "destroy": rc, "info": info}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
+def stall_rank(rank, n, port, env, out_q, call_allreduce):
+    """Timeout test: rank 0 calls all-reduce, the other ranks never do."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        hip_rt.set_device(0)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        buf = hip_rt.DeviceBuffer(1 << 20)
+        res = {}
+        if call_allreduce:
+            t0 = time.time()
+            res["rc"] = comm.all_reduce(buf.ptr, buf.ptr, (1 << 20) // 4, M.ncclFloat, M.ncclSum, 0)
+            res["secs"] = time.time() - t0
+            res["rc2"] = comm.all_reduce(buf.ptr, buf.ptr, (1 << 20) // 4, M.ncclFloat, M.ncclSum, 0)
+            res["async"] = comm.async_error()
+        else:
+            time.sleep(float(env.get("STALL_SECS", "4")))
+        out_q.put((rank, res))
+        buf.free()
+        comm.destroy()
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
+def run_ranks(target, n, args_for_rank, timeout):
+    """Spawn n rank processes, collect one result each; kill stragglers at the deadline."""
+    import multiprocessing as mp
+    # forkserver: children fork from a server started before this process touched the GPU
+    # (conftest starts it), so no child is forked from a GPU-initialised process and
+    # nothing exec()s after HIP init
+    ctx = mp.get_context("forkserver")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=args_for_rank(r) + (q,)) for r in range(n)]
+    for p in procs:
+        p.start()
+    out = {}
+    deadline = time.time() + timeout
+    try:
+        while len(out) < n and time.time() < deadline:
+            try:
+                r, res = q.get(timeout=max(0.1, min(5.0, deadline - time.time())))
+                out[r] = res
+            except Exception:
+                if all(not p.is_alive() for p in procs) and q.empty():
+                    break
+    finally:
+        for p in procs:
+            p.join(timeout=max(1.0, deadline - time.time()) if len(out) == n else 1.0)
+            if p.is_alive():
+                p.kill()
+                p.join(5)
+    return out
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port

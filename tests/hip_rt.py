@@ -1,0 +1,102 @@
+"""Minimal ctypes view of the HIP runtime (libamdhip64.so) for the GPU tests.
+
+Device memory, copies and streams only -- plumbing, so the parity tests exercise
+libmini_nccl.so through its C ABI exactly as a C caller would, without torch.
+"""
+import ctypes
+
+import numpy as np
+
+hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice = 1, 2, 3
+_hip = None
+
+
+def lib():
+    global _hip
+    if _hip is None:
+        try:
+            _hip = ctypes.CDLL("libamdhip64.so")
+        except OSError:
+            _hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+        vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        _hip.hipSetDevice.argtypes = [i]
+        _hip.hipGetDeviceCount.argtypes = [ctypes.POINTER(i)]
+        _hip.hipMalloc.argtypes = [ctypes.POINTER(vp), sz]
+        _hip.hipFree.argtypes = [vp]
+        _hip.hipMemcpy.argtypes = [vp, vp, sz, i]
+        _hip.hipMemset.argtypes = [vp, i, sz]
+        _hip.hipDeviceSynchronize.argtypes = []
+        _hip.hipStreamCreate.argtypes = [ctypes.POINTER(vp)]
+        _hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_uint]
+        _hip.hipStreamSynchronize.argtypes = [vp]
+        _hip.hipStreamDestroy.argtypes = [vp]
+        _hip.hipGetErrorString.argtypes = [i]
+        _hip.hipGetErrorString.restype = ctypes.c_char_p
+        for f in ("hipSetDevice", "hipGetDeviceCount", "hipMalloc", "hipFree", "hipMemcpy", "hipMemset",
+                  "hipDeviceSynchronize", "hipStreamCreate", "hipStreamCreateWithFlags", "hipStreamSynchronize",
+                  "hipStreamDestroy"):
+            getattr(_hip, f).restype = i
+    return _hip
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what}: {lib().hipGetErrorString(rc).decode()} ({rc})")
+
+
+def device_count():
+    n = ctypes.c_int()
+    rc = lib().hipGetDeviceCount(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def set_device(d):
+    check(lib().hipSetDevice(d), "hipSetDevice")
+
+
+class DeviceBuffer:
+    def __init__(self, nbytes):
+        self.nbytes = nbytes
+        p = ctypes.c_void_p()
+        check(lib().hipMalloc(ctypes.byref(p), max(nbytes, 16)), "hipMalloc")
+        self.ptr = p.value
+
+    def upload(self, arr, offset=0):
+        a = np.ascontiguousarray(arr)
+        check(lib().hipMemcpy(self.ptr + offset, a.ctypes.data, a.nbytes, hipMemcpyHostToDevice), "H2D")
+
+    def download(self, dtype, count, offset=0):
+        out = np.empty(count, dtype=dtype)
+        check(lib().hipMemcpy(out.ctypes.data, self.ptr + offset, out.nbytes, hipMemcpyDeviceToHost), "D2H")
+        return out
+
+    def fill_byte(self, value):
+        check(lib().hipMemset(self.ptr, value, self.nbytes), "hipMemset")
+
+    def free(self):
+        if self.ptr:
+            lib().hipFree(self.ptr)
+            self.ptr = 0
+
+
+class Stream:
+    """A non-blocking stream (hipStreamNonBlocking): it does not synchronise with the legacy
+    null stream, so a synchronous hipMemcpy issued by one rank-thread of a process cannot
+    wait behind another rank-thread's running all-reduce kernel."""
+
+    def __init__(self):
+        s = ctypes.c_void_p()
+        check(lib().hipStreamCreateWithFlags(ctypes.byref(s), 1), "hipStreamCreateWithFlags")
+        self.handle = s.value
+
+    def sync(self):
+        check(lib().hipStreamSynchronize(self.handle), "hipStreamSynchronize")
+
+    def destroy(self):
+        if self.handle:
+            lib().hipStreamDestroy(self.handle)
+            self.handle = None
+
+
+def sync():
+    check(lib().hipDeviceSynchronize(), "hipDeviceSynchronize")

@@ -1,0 +1,56 @@
+"""ctypes front end of mini-nccl_amd/lib/libmnccl_sim.so (CPU-only test library).
+
+The simulator executes the GPU kernels' per-channel op sequence (csrc/schedule.h, the
+same header kernels.hip includes) on simulated ranks; see csrc/sim.cpp.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "mini-nccl_amd", "lib", "libmnccl_sim.so")
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        L = ctypes.CDLL(LIB)
+        vp, u64, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+        L.mnccl_sim_allreduce.argtypes = [i, ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64, i, i, i, u64,
+                                          ctypes.POINTER(u64)]
+        L.mnccl_bootstrap_selftest.argtypes = [i, i, ctypes.c_char_p, i, i]
+        L.mnccl_config_describe.argtypes = [ctypes.c_char_p, i]
+        _lib = L
+    return _lib
+
+
+def allreduce(inputs, algo=0, op=0, slice_bytes=1024, channels=4, slots=2, calls=1, seed=0, algos=None):
+    """fp32 all-reduce of `inputs` (one array per rank) through the simulated kernels,
+    `calls` times on one communicator state (schedule `algo` for every call, or the
+    per-call list `algos`).  Returns (outputs, steps); raises RuntimeError on deadlock."""
+    if algos is not None:
+        calls = len(algos)
+        mask = sum((a & 1) << i for i, a in enumerate(algos))
+    else:
+        mask = (1 << calls) - 1 if algo == 1 else 0
+    n = len(inputs)
+    sends = [np.ascontiguousarray(x, dtype=np.float32) for x in inputs]
+    recvs = [np.full_like(x, np.nan) for x in sends]
+    sp = (ctypes.c_void_p * n)(*[s.ctypes.data for s in sends])
+    rp = (ctypes.c_void_p * n)(*[r.ctypes.data for r in recvs])
+    steps = ctypes.c_uint64()
+    rc = load().mnccl_sim_allreduce(mask, sp, rp, n, sends[0].size, op, slice_bytes, channels, slots, calls, seed,
+                                    ctypes.byref(steps))
+    if rc == -1:
+        raise RuntimeError("simulated protocol deadlocked")
+    if rc != 0:
+        raise ValueError(f"bad simulator arguments (rc={rc})")
+    return recvs, steps.value
+
+
+def config_describe(env=None):
+    buf = ctypes.create_string_buffer(512)
+    rc = load().mnccl_config_describe(buf, 512)
+    return rc, buf.value.decode()

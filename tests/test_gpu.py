@@ -1,0 +1,146 @@
+"""GPU parity tests (-m gpu): the HIP path through the C ABI vs the CPU oracle.
+
+* mncclLocalReduce (the scatter-reduce element-wise kernel alone) vs oracle_reduce,
+  every dtype x op, vector and scalar (misaligned / odd-size) paths, bit-exact;
+* ncclAllReduce with 2-4 rank processes sharing GPU 0 (as the reference's perf_test
+  does, tests/perf_test.cpp:46), ring and direct schedules, in/out of place, odd
+  counts (tail), repeated calls, slices smaller than a chunk, bit-exact vs the oracle
+  (NaN payloads of +/* excepted: NaN-ness must match);
+* error paths: watchdog timeout -> ncclInternalError and a sticky error afterwards.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import gpu_workers as GW
+import oracle_api as O
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = ["f32", "f64", "i32", "f16", "bf16"]
+OPS = ["sum", "prod", "max", "min"]
+
+
+@pytest.fixture(scope="module")
+def dev(nccl_lib, oracle_lib):
+    import hip_rt
+    if hip_rt.device_count() < 1:
+        pytest.fail("no HIP device visible: the -m gpu suite must run on the MI355X box")
+    hip_rt.set_device(0)
+    return hip_rt
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("op", OPS)
+@pytest.mark.parametrize("count,offset", [(1 << 20, 0), (100003, 0), (4099, 4), (17, 2)])
+def test_local_reduce_parity(dev, dtype, op, count, offset):
+    import mini_nccl as M
+    code, npd = O.DTYPES[dtype]
+    a, b = GW.make_inputs(2, count, dtype, seed=count + 7, special=op in ("max", "min"))
+    exp = O.reduce(a, b, dtype, op)
+    esz = np.dtype(npd).itemsize
+    off = offset * esz if offset else 0
+    da, db, dc = (dev.DeviceBuffer(count * esz + off) for _ in range(3))
+    da.upload(a, off)
+    db.upload(b, off)
+    rc = M.local_reduce(dc.ptr + off, da.ptr + off, db.ptr + off, count, code, O.OPS[op], 0)
+    assert rc == M.ncclSuccess
+    dev.sync()
+    got = dc.download(npd, count, off)
+    bad, first = GW.compare(got, exp, dtype, op in ("sum", "prod"))
+    assert bad == 0, f"{bad} mismatches, first at {first}: got {got[first]!r} expected {exp[first]!r}"
+    for x in (da, db, dc):
+        x.free()
+
+
+def test_local_reduce_in_place_large(dev):
+    import mini_nccl as M
+    count = 64 << 20  # 256 MiB fp32
+    a, b = GW.make_inputs(2, count, "f32", seed=5, special=False)
+    exp = O.reduce(a, b, "f32", "sum")
+    da, db = dev.DeviceBuffer(a.nbytes), dev.DeviceBuffer(b.nbytes)
+    da.upload(a)
+    db.upload(b)
+    assert M.local_reduce(da.ptr, da.ptr, db.ptr, count, M.ncclFloat, M.ncclSum, 0) == 0
+    dev.sync()
+    assert np.array_equal(da.download(np.float32, count).view(np.uint32), exp.view(np.uint32))
+    da.free()
+    db.free()
+
+
+def _run_allreduce(n, cases, env=None, timeout=300):
+    port = GW.free_port()
+    e = {"MINI_NCCL_TIMEOUT_MS": "20000"}
+    e.update(env or {})
+    out = GW.run_ranks(GW.allreduce_rank, n, lambda r: (r, n, port, cases, e), timeout)
+    assert len(out) == n, f"only ranks {sorted(out)} reported (timeout?)"
+    for r in range(n):
+        assert "error" not in out[r], f"rank {r}:\n{out[r]['error']}"
+        assert out[r]["destroy"] == 0
+        for res in out[r]["results"]:
+            c = res["case"]
+            assert res["rc"] == 0, f"rank {r} case {c}: ncclResult {res['rc']}"
+            assert res["bad"] == 0, f"rank {r} case {c}: {res['bad']} mismatches, first at {res['first']}"
+            assert res["async"] == 0
+    return out
+
+
+def _case(dtype="f32", op="sum", count=1 << 18, inplace=False, algo=0, calls=1, seed=1234, special=False, offset=0):
+    return dict(dtype=dtype, op=op, count=count, inplace=inplace, algo=algo, calls=calls, seed=seed, special=special,
+                offset=offset)
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_allreduce_fp32_sum(dev, n, algo):
+    cases = [
+        _case(count=1 << 20, algo=algo),                     # 4 MiB: C1's size
+        _case(count=(1 << 18) + 3, algo=algo, inplace=True),  # tail of count % n
+        _case(count=1000, algo=algo),                        # fewer slices than channels
+        _case(count=n - 1, algo=algo),                       # count < n: copy only
+        _case(count=123457, algo=algo, calls=3, seed=9),     # repeated calls, odd size
+    ]
+    _run_allreduce(n, cases)
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+def test_allreduce_dtypes_ops(dev, algo):
+    cases = [_case(dtype=d, op=o, count=50000 + 7 * i, algo=algo, seed=100 + i, special=o in ("max", "min"))
+             for i, (d, o) in enumerate((d, o) for d in DTYPES for o in OPS)]
+    _run_allreduce(3, cases)
+
+
+def test_allreduce_small_slices_many_messages(dev):
+    # 1 KiB slices, 4 channels: thousands of flag hand-offs per call, both schedules
+    cases = [_case(count=(1 << 19) + 5, algo=a, calls=2, seed=77) for a in (0, 1)]
+    _run_allreduce(4, cases, env={"MINI_NCCL_SLICE_SIZE": "1024", "MINI_NCCL_CHANNELS": "4"})
+
+
+def test_allreduce_misaligned_scalar_path(dev):
+    cases = [_case(count=40001, algo=a, offset=4, seed=5) for a in (0, 1)]
+    _run_allreduce(2, cases)
+
+
+def test_allreduce_async_mode(dev):
+    cases = [_case(count=1 << 20, algo=a, calls=4, seed=3) for a in (0, 1)]
+    _run_allreduce(2, cases, env={"MINI_NCCL_BLOCKING": "0"})
+
+
+def test_allreduce_reference_known_answers(dev):
+    # perf_test.cpp: all ranks send 1.0 -> every element == nRanks (the oracle agrees)
+    cases = [dict(_case(count=(16 << 20) // 4, seed=0), known="ones")]
+    out = _run_allreduce(2, cases)
+    assert out[0]["info"]["nranks"] == 2
+
+
+def test_watchdog_timeout_is_internal_error_and_sticky(dev):
+    import mini_nccl as M
+    port = GW.free_port()
+    env = {"MINI_NCCL_TIMEOUT_MS": "1500", "STALL_SECS": "6"}
+    out = GW.run_ranks(GW.stall_rank, 2, lambda r: (r, 2, port, env, r == 0), 120)
+    assert 0 in out and "error" not in out[0], out
+    assert out[0]["rc"] == M.ncclInternalError
+    assert out[0]["secs"] < 15
+    assert out[0]["rc2"] == M.ncclInternalError  # the communicator stays failed
+    assert out[0]["async"] == M.ncclInternalError
