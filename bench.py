@@ -44,7 +44,7 @@ def log(*a):
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle)
-def cpu_baseline(budget_s=12.0):
+def cpu_baseline(budget_s=10.0):
     """The host path, timed on this box's cores: AVX2 a += b over the same 1 GiB (the N=1
     workload), plus the reference's C1 config (2-rank 127.0.0.1 TCP ring, 4 MiB)."""
     import numpy as np
@@ -56,7 +56,7 @@ def cpu_baseline(budget_s=12.0):
     b = np.full(COUNT, 2.0, np.float32)
     t_start = time.time()
     t_mt = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, threads, 1)  # first touch / warm
-    iters = max(1, min(10, int((budget_s * 0.45) / max(t_mt, 1e-3))))
+    iters = max(1, min(400, int((budget_s * 0.6) / max(t_mt, 1e-3))))
     t_mt = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, threads, iters)
     t_st = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, 1, 1)
     ok = L.oracle_verify_avx2(a.ctypes.data, COUNT, float(1.0 + 2.0 * (2 + iters))) == -1
@@ -106,6 +106,16 @@ def cpu_baseline(budget_s=12.0):
 
 
 # ------------------------------------------------------------------ helpers
+def reduce_max(dist, x):
+    """max over ranks of a host scalar through the harness's (gloo) process group"""
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def pmc_traffic(key):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/pmc_summary.json)."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -126,6 +136,8 @@ def main():
     ap.add_argument("--algo", choices=["ring", "direct"], default=os.environ.get("MINI_NCCL_ALGO", "ring"))
     ap.add_argument("--no-alt", action="store_true", help="N>1: skip the second schedule and the RCCL reference")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank on GPU 0 (as the reference's perf_test)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -146,6 +158,8 @@ def main():
     import torch
     import mini_nccl as M
     M.load()
+    if args.same_device:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist = None
@@ -161,11 +175,7 @@ def main():
         torch.cuda.synchronize()
 
     def max_over_ranks(x):
-        if dist is None:
-            return x
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return reduce_max(dist, x)
 
     stream = torch.cuda.Stream(device=dev)
     count = args.count

@@ -98,7 +98,7 @@ def allreduce_rank(rank, n, port, cases, env, out_q):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
-def stall_rank(rank, n, port, env, out_q, call_allreduce):
+def stall_rank(rank, n, port, env, call_allreduce, out_q):
     """Timeout test: rank 0 calls all-reduce, the other ranks never do."""
     try:
         os.environ.update(env)

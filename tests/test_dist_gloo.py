@@ -1,0 +1,62 @@
+"""Multi-process paths on the CPU (world_size 2, gloo): the bench harness's barrier /
+max-over-ranks, the TCP bootstrap across processes, and the reference's C1 configuration
+(2-rank 127.0.0.1 TCP ring with AVX2 adds, oracle/ring_oracle.c) checked bit-exactly against
+the oracle -- the N > 1 host-side plumbing without a GPU."""
+import os
+import sys
+import time
+import traceback
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _rank_main(rank, world, master_port, ring_port, boot_port, out_q):
+    try:
+        sys.path[:0] = [HERE, ROOT, os.path.join(ROOT, "mini-nccl_amd")]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(master_port))
+        import ctypes
+
+        import torch.distributed as dist
+
+        import bench
+        import oracle_api as O
+        import sim_api as S
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        res = {}
+        # bench.py's harness: barrier, then max over ranks of a per-rank time
+        dist.barrier()
+        res["max"] = bench.reduce_max(dist, 10.0 + rank)
+        # bootstrap star across processes (the communicator's init path, no GPU)
+        res["boot"] = S.load().mnccl_bootstrap_selftest(rank, world, b"127.0.0.1", boot_port, 20000)
+        # C1: the CPU ring over TCP, one process per rank, random fp32 -> bit-exact vs oracle
+        count = (4 << 20) // 4 + 3
+        xs = O.random_inputs(world, count, "f32", seed=42)
+        exp = O.allreduce(xs, "f32", "sum", slice_bytes=131072)[rank]
+        buf = xs[rank].copy()
+        sec = ctypes.c_double()
+        rc = O.load().oracle_cpu_ring_tcp(rank, world, b"127.0.0.1", ring_port, buf.ctypes.data, count, 131072, 1,
+                                          ctypes.byref(sec))
+        res["ring_rc"] = rc
+        res["ring_exact"] = bool(np.array_equal(buf.view(np.uint32), exp.view(np.uint32)))
+        dist.barrier()
+        dist.destroy_process_group()
+        out_q.put((rank, res))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_world2_harness_bootstrap_and_c1_ring(oracle_lib, sim_lib, world):
+    import gpu_workers as GW
+    ports = [GW.free_port() for _ in range(3)]
+    out = GW.run_ranks(_rank_main, world, lambda r: (r, world, *ports), 120)
+    assert sorted(out) == list(range(world)), out
+    for r in range(world):
+        assert "error" not in out[r], out[r].get("error")
+        assert out[r]["max"] == 10.0 + world - 1
+        assert out[r]["boot"] == 0
+        assert out[r]["ring_rc"] == 0 and out[r]["ring_exact"], out[r]

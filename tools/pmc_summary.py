@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Turn a tools/profile_n1.sh run (gpurun_out/<tag>/) into committed evidence under profiles/.
+
+  python tools/pmc_summary.py <tag> <round>      e.g. prof_n1_r1 r1
+
+Writes
+  profiles/<round>_n1_kernel_stats.csv   rocprofv3 --kernel-trace --stats of `python bench.py`
+                                          (the kernel rows of this library, plus every row's totals)
+  profiles/<round>_n1_pmc.csv            per-dispatch FETCH_SIZE / WRITE_SIZE of this library's kernels
+  profiles/pmc_summary.json              per-launch HBM bytes read by bench.py's roofline.traffic
+
+gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE / WRITE_SIZE are in KiB
+(x 1024); FETCH_SIZE counts exactly half of the bytes of a wide coalesced streaming read
+(16 B per lane), so it is doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.
+"""
+import csv
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def rows(path):
+    with open(path, newline="") as f:
+        return list(csv.DictReader(f))
+
+
+def ours(name):
+    return "mnccl::" in name
+
+
+def main():
+    tag, rnd = sys.argv[1], sys.argv[2]
+    src = os.path.join(ROOT, "gpurun_out", tag)
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+
+    stats = rows(os.path.join(src, "trace", "run_kernel_stats.csv"))
+    with open(os.path.join(prof, f"{rnd}_n1_kernel_stats.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs", "StdDev"])
+        other = [0, 0.0, 0.0]
+        for r in stats:
+            if ours(r["Name"]):
+                w.writerow([r["Name"], r["Calls"], r["TotalDurationNs"], r["AverageNs"], r["Percentage"], r["MinNs"],
+                            r["MaxNs"], r["StdDev"]])
+            else:
+                other[0] += int(r["Calls"])
+                other[1] += float(r["TotalDurationNs"])
+                other[2] += float(r["Percentage"])
+        w.writerow(["(all other kernels: torch fills / checks)", other[0], int(other[1]), "", round(other[2], 2), "", "",
+                    ""])
+
+    per = {}
+    pmc_rows = []
+    for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        for r in rows(os.path.join(src, sub, "run_counter_collection.csv")):
+            if ours(r["Kernel_Name"]) and r["Counter_Name"] == counter:
+                per.setdefault((r["Kernel_Name"], counter), []).append(float(r["Counter_Value"]))
+                pmc_rows.append([r["Kernel_Name"], r["Dispatch_Id"], r["Grid_Size"], r["Workgroup_Size"],
+                                 r["VGPR_Count"], r["SGPR_Count"], counter, r["Counter_Value"]])
+    with open(os.path.join(prof, f"{rnd}_n1_pmc.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Dispatch_Id", "Grid_Size", "Workgroup_Size", "VGPR_Count", "SGPR_Count",
+                    "Counter_Name", "Counter_Value_KiB"])
+        w.writerows(pmc_rows)
+
+    out_path = os.path.join(prof, "pmc_summary.json")
+    summary = json.load(open(out_path)) if os.path.exists(out_path) else {}
+    for kname in sorted({k for k, _ in per}):
+        if "local_reduce_vec<float, 0>" not in kname:
+            continue
+        fetch = per.get((kname, "FETCH_SIZE"), [])
+        write = per.get((kname, "WRITE_SIZE"), [])
+        f_b = 2 * 1024 * sum(fetch) / len(fetch)
+        w_b = 1024 * sum(write) / len(write)
+        alg = 3 * 268435456 * 4
+        summary["local_reduce_f32_1GiB"] = {
+            "kernel": kname,
+            "hbm_bytes_per_launch": int(round(f_b + w_b)),
+            "read_bytes_per_launch": int(round(f_b)),
+            "write_bytes_per_launch": int(round(w_b)),
+            "algorithmic_bytes_per_launch": alg,
+            "traffic_over_algorithmic": round((f_b + w_b) / alg, 4),
+            "dispatches": [len(fetch), len(write)],
+            "source": f"profiles/{rnd}_n1_pmc.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
+                      "FETCH x2 and KiB x1024 per MI355X_MICROARCH.md)",
+        }
+    json.dump(summary, open(out_path, "w"), indent=1, sort_keys=True)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()
