@@ -132,8 +132,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=20)   # perf_test.cpp:93-99: 20 timed
     ap.add_argument("--warmup", type=int, default=5)   # perf_test.cpp:86-90: 5 warm-up
-    ap.add_argument("--count", type=int, default=COUNT)
-    ap.add_argument("--algo", choices=["ring", "direct"], default=os.environ.get("MINI_NCCL_ALGO", "ring"))
+    ap.add_argument("--count", type=int, default=0, help="elements (default: 1 GiB of --dtype)")
+    ap.add_argument("--dtype", choices=["f32", "bf16", "f16"], default="f32",
+                    help="f32 = the headline; bf16/f16 = BASELINE.json configs[4] (C5)")
+    ap.add_argument("--algo", choices=["auto", "ring", "direct"], default=os.environ.get("MINI_NCCL_ALGO", "auto"),
+                    help="auto = the library default (ring at 2 ranks, direct from 3: same bits, every link)")
     ap.add_argument("--no-alt", action="store_true", help="N>1: skip the second schedule and the RCCL reference")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--same-device", action="store_true",
@@ -148,7 +151,7 @@ def main():
     n = world
 
     cpu = None
-    if n == 1 and rank == 0 and not args.no_cpu_baseline:
+    if n == 1 and rank == 0 and not args.no_cpu_baseline and args.dtype == "f32":
         try:
             cpu = cpu_baseline()  # before the GPU is touched
             log("cpu baseline:", json.dumps(cpu))
@@ -178,10 +181,14 @@ def main():
         return reduce_max(dist, x)
 
     stream = torch.cuda.Stream(device=dev)
-    count = args.count
-    nbytes = count * 4
-    result = {"metric": METRIC, "unit": "GB/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
-              "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic"}
+    tdt, ndt, esz = {"f32": (torch.float32, M.ncclFloat, 4), "bf16": (torch.bfloat16, M.ncclBfloat16, 2),
+                     "f16": (torch.float16, M.ncclFloat16, 2)}[args.dtype]
+    count = args.count or (COUNT * 4) // esz
+    nbytes = count * esz
+    metric = METRIC if args.dtype == "f32" else METRIC.replace("fp32", args.dtype)
+    result = {"metric": metric, "unit": "GB/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+              "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+              "data": "synthetic"}
 
     def timed(step_fn, k):
         """K steps between barrier+sync; returns (wall s, mean per-launch event ms)."""
@@ -201,20 +208,20 @@ def main():
     if n == 1:
         g = torch.Generator(device=dev)
         g.manual_seed(1234)
-        a = torch.rand(count, device=dev, generator=g, dtype=torch.float32)
-        b = torch.rand(count, device=dev, generator=g, dtype=torch.float32)
+        a = torch.rand(count, device=dev, generator=g, dtype=torch.float32).to(tdt)
+        b = torch.rand(count, device=dev, generator=g, dtype=torch.float32).to(tdt)
         # parity spot check of one step against torch fp32 (the op is one IEEE add: bit-exact)
         ref = (a[: 1 << 20] + b[: 1 << 20]).clone()
         sh = stream.cuda_stream
 
         def step():
-            rc = M.local_reduce(a.data_ptr(), a.data_ptr(), b.data_ptr(), count, M.ncclFloat, M.ncclSum, sh)
+            rc = M.local_reduce(a.data_ptr(), a.data_ptr(), b.data_ptr(), count, ndt, M.ncclSum, sh)
             if rc != 0:
                 raise M.NcclError(rc, "mncclLocalReduce")
 
         step()
         torch.cuda.synchronize()
-        exact = bool(torch.equal(a[: 1 << 20], ref))
+        exact = bool(torch.equal(a[: 1 << 20], ref))  # one IEEE add (bf16/f16: correctly rounded) per element
         for _ in range(args.warmup):
             step()
         wall, ev_ms = timed(step, args.steps)
@@ -223,21 +230,24 @@ def main():
         result.update({
             "value": round(nbytes / (ms / 1e3) / 1e9, 3),
             "ms_per_step": round(ms, 4),
-            "config": {"workload": "1-GPU local reduce a <- a + b, 1 GiB fp32 (BASELINE.md row '1-GPU local reduce')",
-                       "count": count, "bytes": nbytes, "kernel": "local_reduce_vec<float,Sum>", "parity_step_exact": exact},
+            "config": {"workload": f"1-GPU local reduce a <- a + b, 1 GiB {args.dtype} (BASELINE.md row '1-GPU local reduce')",
+                       "count": count, "bytes": nbytes, "kernel": f"local_reduce_vec<{args.dtype},Sum>",
+                       "parity_step_exact": exact},
         })
-        traffic, tsrc = pmc_traffic("local_reduce_f32_1GiB")
+        traffic, tsrc = pmc_traffic(f"local_reduce_{args.dtype}_1GiB")
         kern_key = "local_reduce_vec"
     else:
         comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
         info = comm.info()
-        send = torch.ones(count, device=dev, dtype=torch.float32)
-        recv = torch.empty(count, device=dev, dtype=torch.float32)
+        if args.algo == "auto":
+            args.algo = "direct" if info["algo"] == M.ALGO_DIRECT else "ring"
+        send = torch.ones(count, device=dev, dtype=tdt)
+        recv = torch.empty(count, device=dev, dtype=tdt)
         sh = stream.cuda_stream
 
         def make_step():
             def step():
-                rc = comm.all_reduce(send.data_ptr(), recv.data_ptr(), count, M.ncclFloat, M.ncclSum, sh)
+                rc = comm.all_reduce(send.data_ptr(), recv.data_ptr(), count, ndt, M.ncclSum, sh)
                 if rc != 0:
                     raise M.NcclError(rc, "ncclAllReduce")
             return step
@@ -259,11 +269,12 @@ def main():
         wall, ev_ms, ok = run_algo(args.algo)
         ms = wall / args.steps * 1e3
         algbw = nbytes / (ms / 1e3) / 1e9
-        alg_bytes = 3 * 4 * (n - 1) * (count // n)
+        alg_bytes = 3 * esz * (n - 1) * (count // n)
         result.update({
             "value": round(algbw, 3),
             "ms_per_step": round(ms, 4),
-            "config": {"workload": f"{n}-rank ring all-reduce, 1 GiB fp32 per rank, HIP IPC over xGMI",
+            "config": {"workload": f"{n}-rank all-reduce (reference ring association), 1 GiB {args.dtype} per rank, "
+                                   f"HIP IPC over xGMI, {args.algo} schedule",
                        "count": count, "bytes": nbytes, "algo": args.algo, "slice_bytes": info["slice_bytes"],
                        "channels": info["channels"], "slots": info["slots"], "threads": info["threads"],
                        "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED"},
@@ -279,7 +290,7 @@ def main():
             except Exception as e:
                 result["alt"] = {"algo": other, "error": str(e)}
             comm.set_algo(M.ALGO_DIRECT if args.algo == "direct" else M.ALGO_RING)
-        traffic, tsrc = pmc_traffic(f"{args.algo}_f32_1GiB_n{n}")
+        traffic, tsrc = pmc_traffic(f"{args.algo}_{args.dtype}_1GiB_n{n}")
         kern_key = f"{args.algo}_kernel"
     achieved = alg_bytes / (ev_ms / 1e3) / 1e9
     result["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -292,7 +303,7 @@ def main():
         try:
             import torch.distributed as dist_
             pg = dist_.new_group(backend="nccl")
-            x = torch.ones(count, device=dev, dtype=torch.float32)
+            x = torch.ones(count, device=dev, dtype=tdt)
             for _ in range(max(1, args.warmup)):
                 dist_.all_reduce(x, group=pg)
             torch.cuda.synchronize()

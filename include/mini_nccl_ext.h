@@ -26,17 +26,17 @@ extern "C" {
 /* schedules; both produce bit-identical results (same fold order per element) */
 typedef enum {
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
-  mncclAlgoDirect = 1  /* owner of chunk c pulls nothing: every peer pushes its chunk-c slice
-                          straight to c over its own xGMI link; c folds in ring order
-                          c, c+1, ..., c-1 and pushes the result to every peer */
+  mncclAlgoDirect = 1  /* every peer pushes its slice of chunk c straight to rank c over its
+                          own xGMI link; c folds them in ring order c, c+1, ..., c-1 and
+                          pushes the result to every peer (default from 3 ranks on) */
 } mncclAlgo_t;
 
 typedef struct {
   int rank, nranks, device;
   size_t slice_bytes;     /* MINI_NCCL_SLICE_SIZE: bytes per channel message */
-  int window;             /* MINI_NCCL_WINDOW_SIZE: messages in flight per link = channels * slots */
+  int window;             /* MINI_NCCL_WINDOW_SIZE: default number of workgroups (channels) */
   int signal_batch;       /* MINI_NCCL_SIGNAL_BATCH (read and validated) */
-  int channels;           /* workgroups of the persistent kernel = independent pipelines */
+  int channels;           /* workgroups of the persistent kernel; each wave is one pipeline */
   int slots;              /* scratch slots per channel (2 = the reference's double buffer) */
   int threads;            /* threads per workgroup */
   int algo;               /* mncclAlgo_t used by ncclAllReduce */

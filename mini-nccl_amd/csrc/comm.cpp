@@ -49,7 +49,9 @@ constexpr uint32_t kInfoMagic = 0x4d4e4931u;  // 'MNI1'
 
 Comm::Comm(int nranks, int rank, const std::string& ip) : rank_(rank), nranks_(nranks) {
   cfg_ = Config::from_env();
-  algo_ = cfg_.algo;
+  // auto: the reference's ring for 2 ranks (one link either way); from 3 ranks on, the
+  // direct schedule, which gives the same bits but uses every xGMI link of the mesh
+  algo_ = cfg_.algo >= 0 ? cfg_.algo : (nranks >= 3 ? 1 : 0);
   if (nranks > kMaxRanks) throw std::invalid_argument("nRanks > 16 is not supported on one node");
   hip_check(hipGetDevice(&device_), "hipGetDevice");
   if (cfg_.debug && rank == 0) fprintf(stderr, "[Config] Loaded: %s\n", cfg_.describe().c_str());
@@ -64,15 +66,17 @@ Comm::Comm(int nranks, int rank, const std::string& ip) : rank_(rank), nranks_(n
 }
 
 void Comm::setup_device_resources() {
-  const int C = cfg_.channels;
-  scratch_bytes_ = (size_t)nranks_ * scratch_region_bytes(C, cfg_.slots, cfg_.slice_size);
+  // one channel per wave: `channels` workgroups x threads/64 waves; the reference's slice
+  // (bytes per channel step) is split across the workgroup's waves
+  const int C = wave_channels();
+  scratch_bytes_ = (size_t)nranks_ * scratch_region_bytes(C, cfg_.slots, wave_slice());
   mbox_bytes_ = (size_t)mbox_words(nranks_, C) * sizeof(uint64_t);
   if (nranks_ > 1) {
     hip_check(hipExtMallocWithFlags((void**)&scratch_, scratch_bytes_, hipDeviceMallocUncached), "alloc scratch");
     hip_check(hipExtMallocWithFlags((void**)&mbox_, mbox_bytes_, hipDeviceMallocUncached), "alloc mailbox");
     hip_check(hipMemset(scratch_, 0, scratch_bytes_), "memset scratch");
     hip_check(hipMemset(mbox_, 0, mbox_bytes_), "memset mailbox");
-    const size_t seq_bytes = (size_t)2 * nranks_ * C * sizeof(uint64_t);
+    const size_t seq_bytes = (size_t)2 * nranks_ * C * sizeof(uint64_t);  // C = wave channels
     hip_check(hipMalloc((void**)&pair_seq_, seq_bytes), "alloc pair_seq");
     hip_check(hipMemset(pair_seq_, 0, seq_bytes), "memset pair_seq");
   }
@@ -281,9 +285,9 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     p.send = (const char*)send;
     p.recv = (char*)recv;
     p.chunk_bytes = chunk_bytes;
-    p.slice_bytes = cfg_.slice_size;
-    p.nslices = (chunk_bytes + cfg_.slice_size - 1) / cfg_.slice_size;
-    const int C = cfg_.channels;
+    p.slice_bytes = wave_slice();
+    p.nslices = (chunk_bytes + p.slice_bytes - 1) / p.slice_bytes;
+    const int C = wave_channels();
     p.iters = (uint32_t)((p.nslices + (uint64_t)C - 1) / (uint64_t)C);
     p.n = n;
     p.rank = rank_;
@@ -301,8 +305,8 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     p.timeout_ticks = (uint64_t)(cfg_.timeout_ms * 1e5);  // s_memrealtime runs at 100 MHz
     p.sys_fence = cfg_.sys_fence;
     const bool vec = (((uintptr_t)send | (uintptr_t)recv) % 16 == 0) && (chunk_bytes % 16 == 0);
-    hipError_t e = algo_ == 1 ? launch_direct(dtype, op, vec, C, cfg_.threads, p, stream)
-                              : launch_ring(dtype, op, vec, C, cfg_.threads, p, stream);
+    hipError_t e = algo_ == 1 ? launch_direct(dtype, op, vec, cfg_.channels, cfg_.threads, p, stream)
+                              : launch_ring(dtype, op, vec, cfg_.channels, cfg_.threads, p, stream);
     hip_check(e, "kernel launch");
   }
   if (cur_dev != device_) hipSetDevice(cur_dev);

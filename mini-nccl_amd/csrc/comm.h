@@ -34,6 +34,9 @@ class Comm {
   void set_algo(int a) { algo_ = a; }
   ncclResult_t async_error();
   size_t scratch_bytes() const { return scratch_bytes_; }
+  // kernel geometry: one pipeline per wave, each moving MINI_NCCL_SLICE_SIZE bytes per message
+  int wave_channels() const { return cfg_.channels * (cfg_.threads / 64); }
+  uint64_t wave_slice() const { return cfg_.slice_size; }
 
  private:
   void setup_device_resources();

@@ -39,10 +39,10 @@ Config Config::from_env() {
   if (c.slots < 2) c.slots = 2;
   if (c.slots > 64) c.slots = 64;
   c.channels = (int)env_int("MINI_NCCL_CHANNELS", 0);
-  if (c.channels <= 0) c.channels = c.window_size / c.slots;
+  if (c.channels <= 0) c.channels = c.window_size;  // workgroups; each wave is one pipeline
   if (c.channels < 1) c.channels = 1;
   if (c.channels > 256) c.channels = 256;
-  c.threads = (int)env_int("MINI_NCCL_THREADS", 512);
+  c.threads = (int)env_int("MINI_NCCL_THREADS", 256);
   if (c.threads < 64) c.threads = 64;
   if (c.threads > 1024) c.threads = 1024;
   c.threads &= ~63;
@@ -50,7 +50,8 @@ Config Config::from_env() {
   if (a && *a) {
     if (!strcmp(a, "ring")) c.algo = 0;
     else if (!strcmp(a, "direct")) c.algo = 1;
-    else throw std::invalid_argument(std::string("MINI_NCCL_ALGO=") + a + " (expected ring|direct)");
+    else if (!strcmp(a, "auto")) c.algo = -1;
+    else throw std::invalid_argument(std::string("MINI_NCCL_ALGO=") + a + " (expected auto|ring|direct)");
   }
   c.blocking = env_int("MINI_NCCL_BLOCKING", 1) != 0;
   c.sys_fence = env_int("MINI_NCCL_SYS_FENCE", 1) != 0;
@@ -67,7 +68,8 @@ std::string Config::describe() const {
   snprintf(b, sizeof b,
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, algo=%s, blocking=%d, "
            "sys_fence=%d, timeout=%.0f ms, port=%d",
-           slice_size, window_size, signal_batch, slots, channels, threads, algo ? "direct" : "ring", blocking,
+           slice_size, window_size, signal_batch, slots, channels, threads,
+           algo < 0 ? "auto" : algo ? "direct" : "ring", blocking,
            sys_fence, timeout_ms, port);
   return b;
 }

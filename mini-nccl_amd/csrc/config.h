@@ -10,13 +10,13 @@ namespace mnccl {
 struct Config {
   // reference knobs, same names and defaults (Config.h:29-51)
   size_t slice_size = 128 * 1024;  // MINI_NCCL_SLICE_SIZE (bytes per channel message; 0 -> 1024)
-  int window_size = 64;            // MINI_NCCL_WINDOW_SIZE (messages in flight per link)
+  int window_size = 64;            // MINI_NCCL_WINDOW_SIZE (workgroups of the persistent kernel)
   int signal_batch = 16;           // MINI_NCCL_SIGNAL_BATCH (validated)
   // this build's knobs
   int slots = 2;                   // MINI_NCCL_SLOTS   scratch slots per channel (>= 2; 2 = double buffer)
-  int channels = 0;                // MINI_NCCL_CHANNELS (0 -> window_size / slots)
-  int threads = 512;               // MINI_NCCL_THREADS threads per workgroup
-  int algo = 0;                    // MINI_NCCL_ALGO    ring | direct
+  int channels = 0;                // MINI_NCCL_CHANNELS (0 -> window_size)
+  int threads = 256;               // MINI_NCCL_THREADS threads per workgroup (one pipeline per wave)
+  int algo = -1;                   // MINI_NCCL_ALGO    auto (-1) | ring (0) | direct (1)
   int blocking = 1;                // MINI_NCCL_BLOCKING host waits for the stream (reference behaviour)
   int sys_fence = 1;               // MINI_NCCL_SYS_FENCE system release fence before each flag
   double timeout_ms = 10000.0;     // MINI_NCCL_TIMEOUT_MS (reference watchdog: 10 s)

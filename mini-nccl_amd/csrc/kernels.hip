@@ -174,7 +174,17 @@ __device__ __forceinline__ void publish(u64* flag, u64 v, int sys_fence) {
   st_sys(flag, v);
 }
 
-// ---------------------------------------------------------------- message bodies
+// ---------------------------------------------------------------- wave-level sync
+// A channel is ONE wave (64 lanes): lane 0 polls and signals, the wave's own s_waitcnt orders
+// its memory operations, and no workgroup barrier is ever needed -- the 16 waves of a
+// workgroup are 16 independent pipelines that hide each other's hand-off latency.
+__device__ __forceinline__ bool wave_wait_ge(const u64* flag, u64 target, const Ctl& c, int lane) {
+  int ok = 1;
+  if (lane == 0) ok = wait_ge(flag, target, c) ? 1 : 0;
+  return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+
+// ---------------------------------------------------------------- message bodies (one wave)
 enum : int { kHasLocal = 1, kHasIn = 2, kWritesRecv = 4, kSends = 8, kReduces = 16 };
 template <int KIND> struct KindBits;
 template <> struct KindBits<kSend> { static constexpr int v = kHasLocal | kSends; };
@@ -183,45 +193,56 @@ template <> struct KindBits<kReduceCopySend> { static constexpr int v = kHasLoca
 template <> struct KindBits<kCopySend> { static constexpr int v = kHasIn | kSends | kWritesRecv; };
 template <> struct KindBits<kCopy> { static constexpr int v = kHasIn | kWritesRecv; };
 
-constexpr int kU = 4;  // 16-byte vectors per lane per sub-block (4 KB .. 16 KB per sub-block)
+constexpr int kU = 8;  // 16-byte vectors per lane per batch: 8 KiB per wave in flight per stream
+
+template <typename T, int OPC, int KIND>
+__device__ __forceinline__ void vec_one(const char* lsrc, char* ldst, rsrc_t in, rsrc_t out, uint32_t i) {
+  constexpr int B = KindBits<KIND>::v;
+  v4u l, x, v;
+  if (B & kHasLocal) l = ld_g16(lsrc + (size_t)i * 16);
+  if (B & kHasIn) x = ld_slot16(in, i * 16);
+  if (B & kReduces) v = reduce16<T, OPC>(l, x);
+  else if (B & kHasIn) v = x;
+  else v = l;
+  if (B & kWritesRecv) st_g16(ldst + (size_t)i * 16, v);
+  if (B & kSends) st_slot16(out, i * 16, v);
+}
 
 template <typename T, int OPC, int KIND>
 __device__ __forceinline__ void move_vec(const char* __restrict__ lsrc, char* __restrict__ ldst, rsrc_t in,
-                                         rsrc_t out, uint32_t nbytes, int tid, int nt) {
+                                         rsrc_t out, uint32_t nbytes, int lane) {
   constexpr int B = KindBits<KIND>::v;
   const uint32_t nvec = nbytes >> 4;
-  for (uint32_t b = 0; b < nvec; b += (uint32_t)nt * kU) {
+  uint32_t b = 0;
+  for (; b + 64 * kU <= nvec; b += 64 * kU) {  // full batches: every lane issues kU loads per stream
     v4u l[kU], x[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const uint32_t i = b + (uint32_t)(u * nt + tid);
-      if (i < nvec) {
-        if (B & kHasLocal) l[u] = ld_g16(lsrc + (size_t)i * 16);
-        if (B & kHasIn) x[u] = ld_slot16(in, i * 16);
-      }
+      const uint32_t i = b + (uint32_t)(u * 64 + lane);
+      if (B & kHasLocal) l[u] = ld_g16(lsrc + (size_t)i * 16);
+      if (B & kHasIn) x[u] = ld_slot16(in, i * 16);
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const uint32_t i = b + (uint32_t)(u * nt + tid);
-      if (i < nvec) {
-        v4u v;
-        if (B & kReduces) v = reduce16<T, OPC>(l[u], x[u]);
-        else if (B & kHasIn) v = x[u];
-        else v = l[u];
-        if (B & kWritesRecv) st_g16(ldst + (size_t)i * 16, v);
-        if (B & kSends) st_slot16(out, i * 16, v);
-      }
+      const uint32_t i = b + (uint32_t)(u * 64 + lane);
+      v4u v;
+      if (B & kReduces) v = reduce16<T, OPC>(l[u], x[u]);
+      else if (B & kHasIn) v = x[u];
+      else v = l[u];
+      if (B & kWritesRecv) st_g16(ldst + (size_t)i * 16, v);
+      if (B & kSends) st_slot16(out, i * 16, v);
     }
   }
+  for (uint32_t i = b + (uint32_t)lane; i < nvec; i += 64) vec_one<T, OPC, KIND>(lsrc, ldst, in, out, i);
 }
 
 template <typename T, int OPC, int KIND>
 __device__ __forceinline__ void move_scalar(const char* __restrict__ lsrc, char* __restrict__ ldst, rsrc_t in,
-                                            rsrc_t out, uint32_t nbytes, int tid, int nt) {
+                                            rsrc_t out, uint32_t nbytes, int lane) {
   constexpr int B = KindBits<KIND>::v;
   typedef typename Scal<sizeof(T)>::U U;
   const uint32_t ne = nbytes / sizeof(T);
-  for (uint32_t i = tid; i < ne; i += nt) {
+  for (uint32_t i = lane; i < ne; i += 64) {
     U l = 0, x = 0, v;
     if (B & kHasLocal) l = reinterpret_cast<const U*>(lsrc)[i];
     if (B & kHasIn) x = Scal<sizeof(T)>::ld(in, i * (uint32_t)sizeof(T));
@@ -234,24 +255,37 @@ __device__ __forceinline__ void move_scalar(const char* __restrict__ lsrc, char*
 }
 
 template <typename T, int OPC, bool VEC, int KIND>
-__device__ __forceinline__ void move(const char* lsrc, char* ldst, rsrc_t in, rsrc_t out, uint32_t nbytes, int tid,
-                                     int nt) {
-  if (VEC) move_vec<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, tid, nt);
-  else move_scalar<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, tid, nt);
+__device__ __forceinline__ void move(const char* lsrc, char* ldst, rsrc_t in, rsrc_t out, uint32_t nbytes, int lane) {
+  if (VEC) move_vec<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, lane);
+  else move_scalar<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, lane);
 }
 
-__device__ __forceinline__ void abort_peers(const CollParams& p, const int* peers, int npeers) {
-  const int C = gridDim.x;
-  for (int k = 0; k < npeers; ++k) st_sys(p.peer_mbox[peers[k]] + mbox_abort(p.n, C), 1ull);
+__device__ __forceinline__ void abort_peers(const CollParams& p, int C, int a, int b) {
+  st_sys(p.peer_mbox[a] + mbox_abort(p.n, C), 1ull);
+  st_sys(p.peer_mbox[b] + mbox_abort(p.n, C), 1ull);
+}
+
+// channel geometry: one channel per wave
+struct WaveId {
+  int lane, wv, w, C;
+};
+__device__ __forceinline__ WaveId wave_id() {
+  WaveId id;
+  id.lane = threadIdx.x & 63;
+  const int W = blockDim.x >> 6;
+  id.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  id.w = __builtin_amdgcn_readfirstlane(blockIdx.x * W + id.wv);
+  id.C = gridDim.x * W;
+  return id;
 }
 
 // ---------------------------------------------------------------- ring kernel
 template <typename T, int OPC, bool VEC>
 __global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
-  const int w = blockIdx.x, C = gridDim.x, tid = threadIdx.x, nt = blockDim.x;
+  const WaveId id = wave_id();
+  const int lane = id.lane, w = id.w, C = id.C;
   const int n = p.n, r = p.rank, K = p.nslots;
   const int prev = mod_n(r - 1, n), next = mod_n(r + 1, n);
-  __shared__ int s_abort;
   const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks};
   // per-pair message counters: the FIFO to `next` and the FIFO from `prev` on this channel
   u64* tx_ctr = p.tx_seq + (u64)next * C + w;
@@ -272,18 +306,14 @@ __global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
     for (int k = 0; k < nops; ++k) {
       const RingOp o = ring_op(n, r, k);
       const u64 rseq = rx_base + itoff + (u64)o.recv_msg, sseq = tx_base + itoff + (u64)o.send_msg;
-      if (tid == 0) {
-        bool ok = true;
-        if (o.recv_msg >= 0) ok = wait_ge(my_ready, rseq + 1, ctl);
-        if (ok && o.send_msg >= 0 && sseq + 1 > (u64)K) ok = wait_ge(my_credit, sseq + 1 - K, ctl);
-        if (ok && o.recv_msg >= 0) acquire_sys();
-        s_abort = ok ? 0 : 1;
-      }
-      __syncthreads();
-      if (s_abort) {
-        if (tid == 0) { const int pe[2] = {prev, next}; abort_peers(p, pe, 2); }
+      bool ok = true;
+      if (o.recv_msg >= 0) ok = wave_wait_ge(my_ready, rseq + 1, ctl, lane);
+      if (ok && o.send_msg >= 0 && sseq + 1 > (u64)K) ok = wave_wait_ge(my_credit, sseq + 1 - K, ctl, lane);
+      if (!ok) {
+        if (lane == 0) abort_peers(p, C, prev, next);
         return;
       }
+      if (o.recv_msg >= 0) acquire_sys();
       if (len) {
         const u64 coff = (u64)o.chunk * p.chunk_bytes + soff;
         const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, prev, w, rseq), len);
@@ -291,22 +321,21 @@ __global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
         const char* lsrc = p.send + coff;
         char* ldst = p.recv + coff;
         switch (o.kind) {
-          case kSend: move<T, OPC, VEC, kSend>(lsrc, ldst, in, out, len, tid, nt); break;
-          case kReduceSend: move<T, OPC, VEC, kReduceSend>(lsrc, ldst, in, out, len, tid, nt); break;
-          case kReduceCopySend: move<T, OPC, VEC, kReduceCopySend>(lsrc, ldst, in, out, len, tid, nt); break;
-          case kCopySend: move<T, OPC, VEC, kCopySend>(lsrc, ldst, in, out, len, tid, nt); break;
-          default: move<T, OPC, VEC, kCopy>(lsrc, ldst, in, out, len, tid, nt); break;
+          case kSend: move<T, OPC, VEC, kSend>(lsrc, ldst, in, out, len, lane); break;
+          case kReduceSend: move<T, OPC, VEC, kReduceSend>(lsrc, ldst, in, out, len, lane); break;
+          case kReduceCopySend: move<T, OPC, VEC, kReduceCopySend>(lsrc, ldst, in, out, len, lane); break;
+          case kCopySend: move<T, OPC, VEC, kCopySend>(lsrc, ldst, in, out, len, lane); break;
+          default: move<T, OPC, VEC, kCopy>(lsrc, ldst, in, out, len, lane); break;
         }
       }
-      if (o.send_msg >= 0) drain_stores();
-      __syncthreads();
-      if (tid == 0) {
+      drain_stores();  // every load of the slot has returned and every store has landed
+      if (lane == 0) {
         if (o.send_msg >= 0) publish(out_ready, sseq + 1, p.sys_fence);
         if (o.recv_msg >= 0) st_sys(out_credit, rseq + 1);
       }
     }
   }
-  if (tid == 0) {
+  if (lane == 0) {
     *tx_ctr = tx_base + (u64)p.iters * mpi;
     *rx_ctr = rx_base + (u64)p.iters * mpi;
   }
@@ -318,17 +347,17 @@ __global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
 // rx0[q]: sequence number of q's raw message for this slice; tx1[d]: of my result message to d
 template <typename T, int OPC, bool VEC>
 __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* lsrc, char* ldst, const u64* rx0,
-                                              const u64* tx1, uint32_t nbytes, int w, int tid, int nt) {
-  const int n = p.n, r = p.rank, C = gridDim.x, K = p.nslots;
+                                              const u64* tx1, uint32_t nbytes, int w, int C, int lane) {
+  const int n = p.n, r = p.rank, K = p.nslots;
   if (VEC) {
-    constexpr int U = 2;
+    constexpr int U = 4;
     const uint32_t nvec = nbytes >> 4;
-    for (uint32_t b = 0; b < nvec; b += (uint32_t)nt * U) {
+    for (uint32_t b = 0; b < nvec; b += 64 * U) {
       v4u acc[U], cur[U], nxt[U];
       bool live[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t i = b + (uint32_t)(u * nt + tid);
+        const uint32_t i = b + (uint32_t)(u * 64 + lane);
         live[u] = i < nvec;
         if (live[u]) acc[u] = ld_g16(lsrc + (size_t)i * 16);
       }
@@ -337,7 +366,7 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
         const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q]), nbytes);
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          if (live[u]) cur[u] = ld_slot16(in, (b + (uint32_t)(u * nt + tid)) * 16);
+          if (live[u]) cur[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
       }
       for (int k = 1; k < n; ++k) {
         if (k + 1 < n) {
@@ -345,7 +374,7 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
           const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q]), nbytes);
 #pragma unroll
           for (int u = 0; u < U; ++u)
-            if (live[u]) nxt[u] = ld_slot16(in, (b + (uint32_t)(u * nt + tid)) * 16);
+            if (live[u]) nxt[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -355,19 +384,19 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (live[u]) st_g16(ldst + (size_t)(b + (uint32_t)(u * nt + tid)) * 16, acc[u]);
+        if (live[u]) st_g16(ldst + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
       for (int k = 1; k < n; ++k) {
         const int d = direct_peer(n, r, k);
         const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slice_bytes, r, w, tx1[d]), nbytes);
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          if (live[u]) st_slot16(out, (b + (uint32_t)(u * nt + tid)) * 16, acc[u]);
+          if (live[u]) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
       }
     }
   } else {
     typedef typename Scal<sizeof(T)>::U Us;
     const uint32_t ne = nbytes / sizeof(T);
-    for (uint32_t i = tid; i < ne; i += nt) {
+    for (uint32_t i = lane; i < ne; i += 64) {
       T acc = reinterpret_cast<const T*>(lsrc)[i];
       for (int k = 1; k < n; ++k) {
         const int q = direct_peer(n, r, k);
@@ -385,113 +414,118 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
   }
 }
 
+constexpr int kMaxWaves = 16;
+
 template <typename T, int OPC, bool VEC>
 __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
-  const int w = blockIdx.x, C = gridDim.x, tid = threadIdx.x, nt = blockDim.x;
+  const WaveId id = wave_id();
+  const int lane = id.lane, w = id.w, C = id.C, wv = id.wv;
   const int n = p.n, r = p.rank, K = p.nslots;
-  __shared__ int s_abort;
-  __shared__ int s_peers[kMaxRanks];
-  // per-pair FIFO counters at the start of the call; per iteration: raw (+0), result (+1)
-  __shared__ u64 s_tx[kMaxRanks], s_rx[kMaxRanks];
-  __shared__ u64 s_rx0[kMaxRanks], s_tx1[kMaxRanks];
+  // per-wave rows: per-pair FIFO counters at call start, and this iteration's positions
+  __shared__ u64 s_tx[kMaxWaves][kMaxRanks], s_rx[kMaxWaves][kMaxRanks];
+  __shared__ u64 s_rx0[kMaxWaves][kMaxRanks], s_tx1[kMaxWaves][kMaxRanks];
+  u64* tx = s_tx[wv];
+  u64* rx = s_rx[wv];
+  u64* rx0 = s_rx0[wv];
+  u64* tx1 = s_tx1[wv];
   const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks};
   const int mpi = direct_msgs_per_iter();
-  if (tid < n - 1) s_peers[tid] = direct_peer(n, r, tid + 1);
-  if (tid < n) {
-    s_tx[tid] = p.tx_seq[(u64)tid * C + w];
-    s_rx[tid] = p.rx_seq[(u64)tid * C + w];
+  if (lane < n) {
+    tx[lane] = p.tx_seq[(u64)lane * C + w];
+    rx[lane] = p.rx_seq[(u64)lane * C + w];
   }
-  __syncthreads();
+  __builtin_amdgcn_wave_barrier();
 
   for (uint32_t it = 0; it < p.iters; ++it) {
     const u64 s = (u64)it * C + w;
     const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
     const u64 soff = s * p.slice_bytes;
     const u64 itoff = (u64)it * mpi;
-    if (tid < n) {
-      s_rx0[tid] = s_rx[tid] + itoff;
-      s_tx1[tid] = s_tx[tid] + itoff + 1;
+    if (lane < n) {
+      rx0[lane] = rx[lane] + itoff;
+      tx1[lane] = tx[lane] + itoff + 1;
     }
+    __builtin_amdgcn_wave_barrier();
 
-    // Phase A: push my raw slice of chunk d to rank d, for every peer d
+    // Phase A: push my raw slice of chunk d to rank d, for every peer d; one drain for all
+    // n-1 pushes, then the n-1 READY flags
     for (int k = 1; k < n; ++k) {
       const int d = direct_peer(n, r, k);
-      const u64 seq0 = s_tx[d] + itoff;
-      if (tid == 0) {
-        bool ok = true;
-        if (seq0 + 1 > (u64)K) ok = wait_ge(p.mbox + mbox_credit(n, C, d, w), seq0 + 1 - K, ctl);
-        s_abort = ok ? 0 : 1;
-      }
-      __syncthreads();
-      if (s_abort) goto aborted;
+      const u64 seq0 = tx[d] + itoff;
+      if (seq0 + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, d, w), seq0 + 1 - K, ctl, lane)) goto aborted;
       if (len) {
         const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slice_bytes, r, w, seq0), len);
         const u64 coff = (u64)d * p.chunk_bytes + soff;
-        move<T, OPC, VEC, kSend>(p.send + coff, nullptr, out, out, len, tid, nt);
+        move<T, OPC, VEC, kSend>(p.send + coff, nullptr, out, out, len, lane);
       }
-      drain_stores();
-      __syncthreads();
-      if (tid == 0) publish(p.peer_mbox[d] + mbox_ready(C, r, w), seq0 + 1, p.sys_fence);
+    }
+    drain_stores();
+    if (lane == 0) {
+      if (p.sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int k = 1; k < n; ++k) {
+        const int d = direct_peer(n, r, k);
+        st_sys(p.peer_mbox[d] + mbox_ready(C, r, w), tx[d] + itoff + 1);
+      }
     }
 
     // Phase B: wait for the n-1 raw slices of my chunk and for slot credits of the
     // result message at every peer; fold; store; push the result everywhere.
-    if (tid == 0) {
-      bool ok = true;
-      for (int k = 1; k < n && ok; ++k) {
-        const int q = direct_peer(n, r, k);
-        ok = wait_ge(p.mbox + mbox_ready(C, q, w), s_rx0[q] + 1, ctl);
-        if (ok && s_tx1[q] + 1 > (u64)K) ok = wait_ge(p.mbox + mbox_credit(n, C, q, w), s_tx1[q] + 1 - K, ctl);
-      }
-      if (ok) acquire_sys();
-      s_abort = ok ? 0 : 1;
+    for (int k = 1; k < n; ++k) {
+      const int q = direct_peer(n, r, k);
+      if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 1, ctl, lane)) goto aborted;
+      if (tx1[q] + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, q, w), tx1[q] + 1 - K, ctl, lane))
+        goto aborted;
     }
-    __syncthreads();
-    if (s_abort) goto aborted;
+    acquire_sys();
     if (len) {
       const u64 coff = (u64)r * p.chunk_bytes + soff;
-      fold_and_push<T, OPC, VEC>(p, p.send + coff, p.recv + coff, s_rx0, s_tx1, len, w, tid, nt);
+      fold_and_push<T, OPC, VEC>(p, p.send + coff, p.recv + coff, rx0, tx1, len, w, C, lane);
     }
     drain_stores();
-    __syncthreads();
-    if (tid == 0) {
+    if (lane == 0) {
       for (int k = 1; k < n; ++k) {
         const int q = direct_peer(n, r, k);
-        st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), s_rx0[q] + 1);  // raw slot consumed
+        st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), rx0[q] + 1);  // raw slot consumed
       }
+      if (p.sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       for (int k = 1; k < n; ++k) {
         const int d = direct_peer(n, r, k);
-        publish(p.peer_mbox[d] + mbox_ready(C, r, w), s_tx1[d] + 1, p.sys_fence);
+        st_sys(p.peer_mbox[d] + mbox_ready(C, r, w), tx1[d] + 1);
       }
     }
 
-    // Phase C: store every peer's result slice
+    // Phase C: wait for every peer's result slice, store them all, one drain, n-1 credits
     for (int k = 1; k < n; ++k) {
       const int q = direct_peer(n, r, k);
-      const u64 seq1 = s_rx0[q] + 1;
-      if (tid == 0) {
-        const bool ok = wait_ge(p.mbox + mbox_ready(C, q, w), seq1 + 1, ctl);
-        if (ok) acquire_sys();
-        s_abort = ok ? 0 : 1;
-      }
-      __syncthreads();
-      if (s_abort) goto aborted;
-      if (len) {
-        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, seq1), len);
+      if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 2, ctl, lane)) goto aborted;
+    }
+    acquire_sys();
+    if (len) {
+      for (int k = 1; k < n; ++k) {
+        const int q = direct_peer(n, r, k);
+        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q] + 1), len);
         const u64 coff = (u64)q * p.chunk_bytes + soff;
-        move<T, OPC, VEC, kCopy>(nullptr, p.recv + coff, in, in, len, tid, nt);
+        move<T, OPC, VEC, kCopy>(nullptr, p.recv + coff, in, in, len, lane);
       }
-      __syncthreads();
-      if (tid == 0) st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), seq1 + 1);
+    }
+    drain_stores();
+    if (lane == 0) {
+      for (int k = 1; k < n; ++k) {
+        const int q = direct_peer(n, r, k);
+        st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), rx0[q] + 2);
+      }
     }
   }
-  if (tid < n && tid != r) {
-    p.tx_seq[(u64)tid * C + w] = s_tx[tid] + (u64)p.iters * mpi;
-    p.rx_seq[(u64)tid * C + w] = s_rx[tid] + (u64)p.iters * mpi;
+  if (lane < n && lane != r) {
+    p.tx_seq[(u64)lane * C + w] = tx[lane] + (u64)p.iters * mpi;
+    p.rx_seq[(u64)lane * C + w] = rx[lane] + (u64)p.iters * mpi;
   }
   return;
 aborted:
-  if (tid == 0) abort_peers(p, s_peers, n - 1);
+  if (lane == 0)
+    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), 1ull);
 }
 
 // ---------------------------------------------------------------- local reduce

@@ -98,8 +98,9 @@ bool ring_step(World& W, Prog& P) {
   return true;
 }
 
-// One direct op (kernels.hip direct_kernel): k in [0, n-1) phase A, k == n-1 phase B,
-// k in [n, 2n-1) phase C.
+// One direct phase (kernels.hip direct_kernel): k == 0 phase A (all raw pushes, then all READY
+// flags), k == 1 phase B (fold + result pushes), k == 2 phase C (all result copies, then all
+// credits).  A phase publishes nothing until its end, as the kernel's single drain per phase.
 bool direct_step(World& W, Prog& P) {
   const int n = W.n, r = P.r, w = P.w, K = W.K;
   const uint64_t s = (uint64_t)P.it * W.C + w;
@@ -109,17 +110,21 @@ bool direct_step(World& W, Prog& P) {
   // per-pair FIFO positions: raw message of this iteration = +0, result = +1
   auto tx0 = [&](int d) { return W.tx_seq[r][(size_t)d * W.C + w] + itoff; };
   auto rx0 = [&](int q) { return W.rx_seq[r][(size_t)q * W.C + w] + itoff; };
-  if (P.k < n - 1) {
-    const int d = direct_peer(n, r, P.k + 1);
-    const uint64_t seq0 = tx0(d);
-    if (seq0 + 1 > (uint64_t)K && W.credit(r, d, w) < seq0 + 1 - K) return false;
-    if (len) {
-      const uint64_t coff = (uint64_t)d * W.chunk_bytes + soff;
-      do_move(kSend, W.op, (const float*)((const char*)W.send[r] + coff), nullptr, nullptr, (float*)W.slot(d, r, w, seq0),
-              len);
+  if (P.k == 0) {
+    for (int k = 1; k < n; ++k) {
+      const int d = direct_peer(n, r, k);
+      if (tx0(d) + 1 > (uint64_t)K && W.credit(r, d, w) < tx0(d) + 1 - K) return false;
     }
-    W.ready(d, r, w) = seq0 + 1;
-  } else if (P.k == n - 1) {
+    for (int k = 1; k < n; ++k) {
+      const int d = direct_peer(n, r, k);
+      if (len) {
+        const uint64_t coff = (uint64_t)d * W.chunk_bytes + soff;
+        do_move(kSend, W.op, (const float*)((const char*)W.send[r] + coff), nullptr, nullptr,
+                (float*)W.slot(d, r, w, tx0(d)), len);
+      }
+    }
+    for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx0(direct_peer(n, r, k)) + 1;
+  } else if (P.k == 1) {
     for (int k = 1; k < n; ++k) {
       const int q = direct_peer(n, r, k);
       if (W.ready(r, q, w) < rx0(q) + 1) return false;
@@ -145,16 +150,19 @@ bool direct_step(World& W, Prog& P) {
     for (int k = 1; k < n; ++k) W.credit(direct_peer(n, r, k), r, w) = rx0(direct_peer(n, r, k)) + 1;
     for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx0(direct_peer(n, r, k)) + 2;
   } else {
-    const int q = direct_peer(n, r, P.k - n + 1);
-    const uint64_t seq1 = rx0(q) + 1;
-    if (W.ready(r, q, w) < seq1 + 1) return false;
-    if (len) {
-      const uint64_t coff = (uint64_t)q * W.chunk_bytes + soff;
-      do_move(kCopy, W.op, nullptr, (const float*)W.slot(r, q, w, seq1), (float*)((char*)W.recv[r] + coff), nullptr, len);
+    for (int k = 1; k < n; ++k)
+      if (W.ready(r, direct_peer(n, r, k), w) < rx0(direct_peer(n, r, k)) + 2) return false;
+    for (int k = 1; k < n; ++k) {
+      const int q = direct_peer(n, r, k);
+      if (len) {
+        const uint64_t coff = (uint64_t)q * W.chunk_bytes + soff;
+        do_move(kCopy, W.op, nullptr, (const float*)W.slot(r, q, w, rx0(q) + 1), (float*)((char*)W.recv[r] + coff),
+                nullptr, len);
+      }
     }
-    W.credit(q, r, w) = seq1 + 1;
+    for (int k = 1; k < n; ++k) W.credit(direct_peer(n, r, k), r, w) = rx0(direct_peer(n, r, k)) + 2;
   }
-  if (++P.k == 2 * n - 1) {
+  if (++P.k == 3) {
     P.k = 0;
     if (++P.it == W.iters) P.done = true;
   }

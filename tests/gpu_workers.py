@@ -98,6 +98,50 @@ def allreduce_rank(rank, n, port, cases, env, out_q):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def graph_rank(rank, n, port, env, replays, out_q):
+    """Capture one ncclAllReduce into a HIP graph, replay it `replays` times with fresh input
+    each time; the per-pair sequence counters live on the device, so replays stay in step."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        hip_rt.set_device(0)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        st = hip_rt.Stream()
+        count = (1 << 18) + 1
+        send, recv = hip_rt.DeviceBuffer(count * 4), hip_rt.DeviceBuffer(count * 4)
+        rcs = []
+        g = hip_rt.Graph(st, lambda: rcs.append(comm.all_reduce(send.ptr, recv.ptr, count, M.ncclFloat, M.ncclSum,
+                                                                st.handle)))
+        bad = []
+        for k in range(replays):
+            xs = O.random_inputs(n, count, "f32", seed=500 + k)
+            exp = O.allreduce(xs, "f32", "sum")[rank]
+            send.upload(xs[rank])
+            g.launch()
+            st.sync()
+            got = recv.download(np.float32, count)
+            bad.append(int((got.view(np.uint32) != exp.view(np.uint32)).sum()))
+        # an eager call after the replays still lines up with the peers
+        xs = O.random_inputs(n, count, "f32", seed=999)
+        send.upload(xs[rank])
+        rc = comm.all_reduce(send.ptr, recv.ptr, count, M.ncclFloat, M.ncclSum, st.handle)
+        st.sync()
+        got = recv.download(np.float32, count)
+        exp = O.allreduce(xs, "f32", "sum")[rank]
+        g.destroy()
+        out_q.put((rank, {"capture_rc": rcs, "bad": bad, "eager_rc": rc,
+                          "eager_bad": int((got.view(np.uint32) != exp.view(np.uint32)).sum())}))
+        send.free()
+        recv.free()
+        st.destroy()
+        comm.destroy()
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
 def stall_rank(rank, n, port, env, call_allreduce, out_q):
     """Timeout test: rank 0 calls all-reduce, the other ranks never do."""
     try:

@@ -32,6 +32,15 @@ def lib():
         _hip.hipStreamDestroy.argtypes = [vp]
         _hip.hipGetErrorString.argtypes = [i]
         _hip.hipGetErrorString.restype = ctypes.c_char_p
+        _hip.hipStreamBeginCapture.argtypes = [vp, i]
+        _hip.hipStreamEndCapture.argtypes = [vp, ctypes.POINTER(vp)]
+        _hip.hipGraphInstantiate.argtypes = [ctypes.POINTER(vp), vp, vp, ctypes.c_char_p, sz]
+        _hip.hipGraphLaunch.argtypes = [vp, vp]
+        _hip.hipGraphExecDestroy.argtypes = [vp]
+        _hip.hipGraphDestroy.argtypes = [vp]
+        for f in ("hipStreamBeginCapture", "hipStreamEndCapture", "hipGraphInstantiate", "hipGraphLaunch",
+                  "hipGraphExecDestroy", "hipGraphDestroy"):
+            getattr(_hip, f).restype = i
         for f in ("hipSetDevice", "hipGetDeviceCount", "hipMalloc", "hipFree", "hipMemcpy", "hipMemset",
                   "hipDeviceSynchronize", "hipStreamCreate", "hipStreamCreateWithFlags", "hipStreamSynchronize",
                   "hipStreamDestroy"):
@@ -100,3 +109,27 @@ class Stream:
 
 def sync():
     check(lib().hipDeviceSynchronize(), "hipDeviceSynchronize")
+
+
+class Graph:
+    """Capture the HIP work a callable enqueues on `stream` into a graph; replay it with launch()."""
+
+    def __init__(self, stream, fn):
+        self.stream = stream
+        check(lib().hipStreamBeginCapture(stream.handle, 0), "hipStreamBeginCapture")  # global mode
+        try:
+            fn()
+        finally:
+            g = ctypes.c_void_p()
+            check(lib().hipStreamEndCapture(stream.handle, ctypes.byref(g)), "hipStreamEndCapture")
+        self.graph = g.value
+        ex = ctypes.c_void_p()
+        check(lib().hipGraphInstantiate(ctypes.byref(ex), self.graph, None, None, 0), "hipGraphInstantiate")
+        self.exec = ex.value
+
+    def launch(self):
+        check(lib().hipGraphLaunch(self.exec, self.stream.handle), "hipGraphLaunch")
+
+    def destroy(self):
+        lib().hipGraphExecDestroy(self.exec)
+        lib().hipGraphDestroy(self.graph)

@@ -136,8 +136,9 @@ def test_config_from_env(sim_lib, monkeypatch):
             monkeypatch.delenv(k)
     rc, s = S.config_describe()
     assert rc == 0
-    # reference defaults (Config.h:29-47): 128 KiB, 64, 16; channels = window / slots
-    assert "SLICE_SIZE=131072 B" in s and "WINDOW=64" in s and "BATCH=16" in s and "channels=32" in s
+    # reference defaults (Config.h:29-47): 128 KiB, 64, 16; workgroups = window
+    assert "SLICE_SIZE=131072 B" in s and "WINDOW=64" in s and "BATCH=16" in s and "channels=64" in s
+    assert "algo=auto" in s and "threads=256" in s
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", "0")       # Config.h:50: 0 -> 1024
     monkeypatch.setenv("MINI_NCCL_WINDOW_SIZE", "-3")     # Config.h:51: <= 0 -> 1
     monkeypatch.setenv("MINI_NCCL_SLOTS", "1")            # clamped to 2 (deadlock-free minimum)
@@ -147,6 +148,9 @@ def test_config_from_env(sim_lib, monkeypatch):
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", "100")     # rounded down to whole 16-byte vectors
     rc, s = S.config_describe()
     assert "algo=direct" in s and "SLICE_SIZE=96 B" in s
+    monkeypatch.setenv("MINI_NCCL_ALGO", "auto")
+    rc, s = S.config_describe()
+    assert rc == 0 and "algo=auto" in s
     monkeypatch.setenv("MINI_NCCL_ALGO", "tree")
     rc, s = S.config_describe()
     assert rc == -1 and "MINI_NCCL_ALGO" in s

@@ -144,3 +144,18 @@ def test_watchdog_timeout_is_internal_error_and_sticky(dev):
     assert out[0]["secs"] < 15
     assert out[0]["rc2"] == M.ncclInternalError  # the communicator stays failed
     assert out[0]["async"] == M.ncclInternalError
+
+
+@pytest.mark.parametrize("algo", ["ring", "direct"])
+def test_allreduce_hip_graph_capture_and_replay(dev, algo):
+    # the reference only warns under capture (api.cpp:153-166); here a captured all-reduce
+    # replays correctly because the FIFO counters are device state advanced by the kernel
+    port = GW.free_port()
+    env = {"MINI_NCCL_TIMEOUT_MS": "20000", "MINI_NCCL_ALGO": algo}
+    out = GW.run_ranks(GW.graph_rank, 3, lambda r: (r, 3, port, env, 4), 240)
+    assert sorted(out) == [0, 1, 2], out
+    for r in range(3):
+        assert "error" not in out[r], out[r]["error"]
+        assert out[r]["capture_rc"] == [0]
+        assert out[r]["bad"] == [0, 0, 0, 0]
+        assert out[r]["eager_rc"] == 0 and out[r]["eager_bad"] == 0

@@ -64,6 +64,27 @@ __global__ void contig(v4f* out, const v4f* a, const v4f* b, size_t nvec) {
   for (int u = 0; u < U; ++u) if (base + u < nvec) __builtin_nontemporal_store(x[u] + y[u], out + base + u);
 }
 
+// the north star's "LDS staging of the arriving peer slice", measured: (1) through registers,
+// (2) by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip) -- incoming b lands in LDS first
+__global__ void __launch_bounds__(64) lds_reg(v4f* out, const v4f* a, const v4f* b, size_t nvec) {
+  __shared__ v4f tile[64];
+  const size_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= nvec) return;
+  tile[threadIdx.x] = __builtin_nontemporal_load(b + i);
+  const v4f x = __builtin_nontemporal_load(a + i);
+  __syncthreads();
+  __builtin_nontemporal_store(x + tile[threadIdx.x], out + i);
+}
+__global__ void __launch_bounds__(64) lds_dma(v4f* out, const v4f* a, const v4f* b, size_t nvec) {
+  __shared__ v4f tile[64];
+  const size_t i = blockIdx.x * 64 + threadIdx.x;
+  __builtin_amdgcn_global_load_lds((const void*)(b + i), (__attribute__((address_space(3))) void*)tile, 16, 0, 2);
+  const v4f x = __builtin_nontemporal_load(a + i);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  __builtin_nontemporal_store(x + tile[threadIdx.x], out + i);
+}
+
 struct Var { const char* name; void (*launch)(v4f*, const v4f*, const v4f*, size_t); };
 
 template <int U, int NTL, int NTS, int NT, int GRID>
@@ -72,6 +93,8 @@ template <int U, int NTL, int NTS, int NT>
 void Lexact(v4f* o, const v4f* a, const v4f* b, size_t n) { gs<U, NTL, NTS><<<(unsigned)((n + (size_t)NT * U - 1) / ((size_t)NT * U)), NT>>>(o, a, b, n); }
 template <int U, int NT>
 void Lcontig(v4f* o, const v4f* a, const v4f* b, size_t n) { contig<U><<<(unsigned)((n + (size_t)NT * U - 1) / ((size_t)NT * U)), NT>>>(o, a, b, n); }
+void Llds_reg(v4f* o, const v4f* a, const v4f* b, size_t n) { lds_reg<<<(unsigned)((n + 63) / 64), 64>>>(o, a, b, n); }
+void Llds_dma(v4f* o, const v4f* a, const v4f* b, size_t n) { lds_dma<<<(unsigned)(n / 64), 64>>>(o, a, b, n); }
 template <int U, int NTL, int NTS, int NT, int GRID>
 void Lnc(v4f* o, const v4f* a, const v4f* b, size_t n) { gs_nochk<U, NTL, NTS><<<GRID, NT>>>(o, a, b, n); }
 
@@ -83,17 +106,15 @@ int main() {
   CK(hipMemset(a, 0, count * 4));
   CK(hipMemset(b, 0, count * 4));
   std::vector<Var> vs = {
-    {"U4 nt/nt 256x4096 (current)", L<4, 1, 1, 256, 4096>},
-    {"U1 nt/nt 64 exact", Lexact<1, 1, 1, 64>},
-    {"U2 nt/nt 64 exact", Lexact<2, 1, 1, 64>},
-    {"U4 nt/nt 64 exact", Lexact<4, 1, 1, 64>},
+    {"U4 nt/nt 256x4096 grid-stride", L<4, 1, 1, 256, 4096>},
+    {"U4 pl/pl 256x4096 grid-stride", L<4, 0, 0, 256, 4096>},
+    {"U1 nt/nt 64 exact (shipped)", Lexact<1, 1, 1, 64>},
     {"U1 nt/nt 128 exact", Lexact<1, 1, 1, 128>},
-    {"contig U2 64", Lcontig<2, 64>},
-    {"contig U2 256", Lcontig<2, 256>},
-    {"contig U4 64", Lcontig<4, 64>},
-    {"U1 nt/nt 64x262144 gs", L<1, 1, 1, 64, 262144>},
-    {"U2 nt/nt 64x131072 gs", L<2, 1, 1, 64, 131072>},
-    {"U4 nt/nt 64x16384 gs", L<4, 1, 1, 64, 16384>},
+    {"U1 nt/nt 256 exact", Lexact<1, 1, 1, 256>},
+    {"U2 nt/nt 64 exact", Lexact<2, 1, 1, 64>},
+    {"U1 pl/pl 64 exact", Lexact<1, 0, 0, 64>},
+    {"LDS-staged b (registers) 64", Llds_reg},
+    {"LDS-staged b (LDS-DMA) 64", Llds_dma},
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));

@@ -20,14 +20,14 @@ run() {
   [ $rc -eq 124 ] || [ $rc -eq 137 ] && exit 9
   return 0
 }
-for algo in ring direct; do
-  for ch in 8 16 32 64; do
-    for sl in 65536 131072 262144 1048576; do
-      run "algo=$algo ch=$ch slice=$sl" MINI_NCCL_ALGO=$algo MINI_NCCL_CHANNELS=$ch MINI_NCCL_SLICE_SIZE=$sl
+for algo in ${ALGOS:-ring direct}; do
+  for ch in 16 32 64 128; do
+    for thr in 64 256 512; do
+      for sl in 131072 262144 524288; do
+        run "n=$NR algo=$algo ch=$ch thr=$thr slice=$sl" MINI_NCCL_ALGO=$algo MINI_NCCL_CHANNELS=$ch MINI_NCCL_THREADS=$thr MINI_NCCL_SLICE_SIZE=$sl
+      done
     done
   done
-  run "algo=$algo ch=32 slice=131072 fence=0" MINI_NCCL_ALGO=$algo MINI_NCCL_SYS_FENCE=0
-  run "algo=$algo ch=32 slice=131072 thr=256" MINI_NCCL_ALGO=$algo MINI_NCCL_THREADS=256
-  run "algo=$algo ch=32 slice=131072 thr=1024" MINI_NCCL_ALGO=$algo MINI_NCCL_THREADS=1024
-  run "algo=$algo ch=32 slice=131072 slots=4" MINI_NCCL_ALGO=$algo MINI_NCCL_SLOTS=4
+  run "n=$NR algo=$algo defaults fence=0" MINI_NCCL_ALGO=$algo MINI_NCCL_SYS_FENCE=0
+  run "n=$NR algo=$algo defaults slots=4" MINI_NCCL_ALGO=$algo MINI_NCCL_SLOTS=4
 done
