@@ -266,6 +266,16 @@ def main():
             ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
             return max_over_ranks(wall), max_over_ranks(ev_ms), ok
 
+        # the xGMI roofline the schedules are bound by: write bandwidth per link with the hot
+        # path's store form, one link per rank (the ring's) and every link at once (direct's)
+        link = {}
+        try:
+            torch.cuda.synchronize()
+            dist.barrier()
+            link["probe_next_GBps"] = round(max_over_ranks(-comm.link_probe(False, 0, 10)) * -1, 2)
+            link["probe_mesh_GBps_per_link"] = round(max_over_ranks(-comm.link_probe(True, 0, 10)) * -1, 2)
+        except Exception as e:
+            link["error"] = str(e)[:200]
         wall, ev_ms, ok = run_algo(args.algo)
         ms = wall / args.steps * 1e3
         algbw = nbytes / (ms / 1e3) / 1e9
@@ -280,6 +290,15 @@ def main():
                        "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED"},
             "busbw": round(algbw * 2 * (n - 1) / n, 3),
         })
+        # ceiling of each schedule from the probed links (min over ranks): ring moves
+        # 2(n-1)/n of the buffer through one link, direct 2/n through each of n-1 links
+        if "probe_next_GBps" in link:
+            ring_ceiling = link["probe_next_GBps"] * n / (2 * (n - 1))
+            direct_ceiling = link["probe_mesh_GBps_per_link"] * n / 2
+            ceiling = direct_ceiling if args.algo == "direct" else ring_ceiling
+            link.update({"ring_ceiling_GBps": round(ring_ceiling, 2), "direct_ceiling_GBps": round(direct_ceiling, 2),
+                         "frac": round(algbw / ceiling, 4)})
+        result["link"] = link
         if not args.no_alt:
             other = "direct" if args.algo == "ring" else "ring"
             try:

@@ -13,6 +13,7 @@
  *                        call returns this error), like NCCL's ncclCommGetAsyncError.
  *   mncclCommGetInfo     resolved configuration of a communicator.
  *   mncclCommSetAlgo     choose the schedule for later calls (same association order).
+ *   mncclCommLinkProbe   measure the xGMI write bandwidth the schedules are bound by.
  */
 #ifndef MINI_NCCL_EXT_H_
 #define MINI_NCCL_EXT_H_
@@ -54,6 +55,13 @@ ncclResult_t mncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError);
 ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info);
 
 ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo);
+
+/* Collective diagnostic: every rank streams `bytes` (0 = its whole scratch region) into the
+ * next rank's scratch (allPeers = 0: one xGMI link per rank, the ring's) or into every peer's
+ * at once (allPeers = 1: the mesh, the direct schedule's), `iters` times, with the hot path's
+ * store form; *gbps = bytes per second per destination link.  Call only when no all-reduce is
+ * in flight on any rank (it overwrites scratch slots). */
+ncclResult_t mncclCommLinkProbe(ncclComm_t comm, int allPeers, size_t bytes, int iters, double* gbps);
 
 /* library version, 10000*major + 100*minor + patch */
 int mncclVersion(void);

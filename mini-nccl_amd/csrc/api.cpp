@@ -166,6 +166,18 @@ ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo) {
   return ncclSuccess;
 }
 
+ncclResult_t mncclCommLinkProbe(ncclComm_t comm, int allPeers, size_t bytes, int iters, double* gbps) {
+  if (!comm || !gbps) return ncclInvalidArgument;
+  try {
+    return reinterpret_cast<Comm*>(comm)->link_probe(allPeers, bytes, iters, gbps);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "[Mini-NCCL] LinkProbe Error: %s\n", e.what());
+    return ncclInternalError;
+  } catch (...) {
+    return ncclSystemError;
+  }
+}
+
 int mncclVersion(void) { return 100; /* 0.1.0 */ }
 
 }  // extern "C"

@@ -314,6 +314,43 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
   return ncclSuccess;
 }
 
+ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gbps) {
+  if (nranks_ < 2 || iters < 1) return ncclInvalidArgument;
+  const size_t region = scratch_region_bytes(wave_channels(), cfg_.slots, wave_slice());
+  if (bytes == 0 || bytes > region) bytes = region;  // the probe writes this rank's region at each peer
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  char* src = nullptr;
+  hip_check(hipMalloc((void**)&src, bytes), "probe alloc");
+  hip_check(hipMemset(src, 0x5a, bytes), "probe memset");
+  std::vector<char*> dst;
+  for (int k = 1; k < nranks_; ++k) {
+    const int d = (rank_ + k) % nranks_;
+    dst.push_back(peer_scratch_[(size_t)d] + (size_t)rank_ * region);
+    if (!all_peers) break;
+  }
+  hipStream_t st;
+  hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "probe stream");
+  hipEvent_t e0, e1;
+  hip_check(hipEventCreate(&e0), "event");
+  hip_check(hipEventCreate(&e1), "event");
+  hip_check(hipDeviceSynchronize(), "probe sync");
+  boot_.barrier();  // every rank idle and launching together
+  hip_check(launch_link_probe(src, dst.data(), (int)dst.size(), bytes, st), "probe warm-up");
+  hip_check(hipEventRecord(e0, st), "event");
+  for (int i = 0; i < iters; ++i) hip_check(launch_link_probe(src, dst.data(), (int)dst.size(), bytes, st), "probe");
+  hip_check(hipEventRecord(e1, st), "event");
+  hip_check(hipEventSynchronize(e1), "probe wait");
+  float ms = 0;
+  hip_check(hipEventElapsedTime(&ms, e0, e1), "event time");
+  boot_.barrier();  // nobody starts an all-reduce while a peer still writes its slots
+  *gbps = (double)bytes * iters / (ms * 1e-3) / 1e9;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipStreamDestroy(st);
+  hipFree(src);
+  return ncclSuccess;
+}
+
 ncclResult_t local_reduce(void* out, const void* local, const void* incoming, size_t count, int dtype, int op,
                           hipStream_t stream) {
   hip_check(launch_local_reduce(dtype, op, out, local, incoming, count, stream), "local reduce launch");

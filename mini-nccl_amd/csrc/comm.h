@@ -33,6 +33,10 @@ class Comm {
   int algo() const { return algo_; }
   void set_algo(int a) { algo_ = a; }
   ncclResult_t async_error();
+  // Collective: every rank writes `bytes` into the next rank's scratch (all_peers = 0) or into
+  // every peer's scratch at once (1), `iters` times; *gbps = bytes per second per link
+  // direction (max over nothing: this rank's own time).  No all-reduce may be in flight.
+  ncclResult_t link_probe(int all_peers, size_t bytes, int iters, double* gbps);
   size_t scratch_bytes() const { return scratch_bytes_; }
   // kernel geometry: one pipeline per wave, each moving MINI_NCCL_SLICE_SIZE bytes per message
   int wave_channels() const { return cfg_.channels * (cfg_.threads / 64); }

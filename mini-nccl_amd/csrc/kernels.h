@@ -42,6 +42,11 @@ hipError_t launch_direct(int dtype, int op, bool vec, int channels, int threads,
 hipError_t launch_local_reduce(int dtype, int op, void* out, const void* local,
                                const void* incoming, uint64_t count, hipStream_t stream);
 
+// Link probe: every block streams `bytes` from `src` into each destination in `dst[0..ndst)`
+// with the hot path's store form (16-byte system-coherent buffer stores); blocks are spread
+// over destinations.  Used to measure the xGMI bandwidth the schedules are bound by.
+hipError_t launch_link_probe(const char* src, char* const* dst, int ndst, uint64_t bytes, hipStream_t stream);
+
 bool dtype_supported(int dtype);
 int dtype_size(int dtype);
 

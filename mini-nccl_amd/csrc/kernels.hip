@@ -565,6 +565,48 @@ __global__ void __launch_bounds__(256) local_reduce_scalar(T* __restrict__ out, 
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = Op<T, OPC>::f(a[i], b[i]);
 }
 
+// ---------------------------------------------------------------- link probe
+struct ProbeArgs {
+  const char* src;
+  char* dst[kMaxRanks];
+  int ndst;
+  uint64_t bytes;
+};
+
+// blocks [d * per, (d+1) * per) write destination d; 8 x 16 B per lane in flight
+__global__ void __launch_bounds__(256) link_probe_kernel(ProbeArgs a) {
+  const int per = gridDim.x / a.ndst;
+  const int d = blockIdx.x / per, b = blockIdx.x % per;
+  if (d >= a.ndst) return;
+  const uint64_t nvec = a.bytes / 16;
+  const rsrc_t out = make_rsrc(a.dst[d], (uint32_t)a.bytes);
+  for (uint64_t base = (uint64_t)b * 256 * 8 + threadIdx.x; base < nvec; base += (uint64_t)per * 256 * 8) {
+    v4u v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint64_t i = base + (uint64_t)u * 256;
+      if (i < nvec) v[u] = ld_g16(a.src + i * 16);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint64_t i = base + (uint64_t)u * 256;
+      if (i < nvec) st_slot16(out, (uint32_t)(i * 16), v[u]);
+    }
+  }
+}
+
+hipError_t launch_link_probe(const char* src, char* const* dst, int ndst, uint64_t bytes, hipStream_t st) {
+  if (ndst < 1 || ndst > kMaxRanks || bytes == 0 || bytes > 0xffffffffull) return hipErrorInvalidValue;
+  ProbeArgs a;
+  a.src = src;
+  for (int i = 0; i < kMaxRanks; ++i) a.dst[i] = i < ndst ? dst[i] : nullptr;
+  a.ndst = ndst;
+  a.bytes = bytes;
+  const int per = 256 / ndst > 0 ? 256 / ndst : 1;
+  hipLaunchKernelGGL(link_probe_kernel, dim3(per * ndst), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- dispatch
 template <template <typename, int, bool> class K>
 struct Unused {};

@@ -64,6 +64,7 @@ SIGNATURES = {
     "mncclCommGetAsyncError": (_I, [_VP, ctypes.POINTER(_I)]),
     "mncclCommGetInfo": (_I, [_VP, ctypes.POINTER(CommInfo)]),
     "mncclCommSetAlgo": (_I, [_VP, _I]),
+    "mncclCommLinkProbe": (_I, [_VP, _I, _SZ, _I, ctypes.POINTER(ctypes.c_double)]),
     "mncclVersion": (_I, []),
 }
 
@@ -129,6 +130,13 @@ class Comm:
         i = CommInfo()
         check(load().mncclCommGetInfo(self.handle, ctypes.byref(i)))
         return {f: getattr(i, f) for f, _ in CommInfo._fields_}
+
+    def link_probe(self, all_peers=False, nbytes=0, iters=10):
+        """GB/s per destination link (collective: every rank must call it)."""
+        g = ctypes.c_double()
+        check(load().mncclCommLinkProbe(self.handle, int(bool(all_peers)), nbytes, iters, ctypes.byref(g)),
+              "mncclCommLinkProbe")
+        return g.value
 
     def set_algo(self, algo):
         return check(load().mncclCommSetAlgo(self.handle, algo))

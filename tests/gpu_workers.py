@@ -142,6 +142,34 @@ def graph_rank(rank, n, port, env, replays, out_q):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def probe_rank(rank, n, port, env, out_q):
+    """mncclCommLinkProbe is collective; afterwards an all-reduce must still be correct
+    (the probe overwrote scratch slots while no message was in flight)."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        hip_rt.set_device(0)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        res = {"next": comm.link_probe(False, 8 << 20, 3), "mesh": comm.link_probe(True, 8 << 20, 3)}
+        count = 100003
+        xs = O.random_inputs(n, count, "f32", seed=3)
+        send, recv = hip_rt.DeviceBuffer(count * 4), hip_rt.DeviceBuffer(count * 4)
+        send.upload(xs[rank])
+        res["rc"] = comm.all_reduce(send.ptr, recv.ptr, count, M.ncclFloat, M.ncclSum, 0)
+        hip_rt.sync()
+        got = recv.download(np.float32, count)
+        res["exact"] = bool(np.array_equal(got.view(np.uint32), O.allreduce(xs)[rank].view(np.uint32)))
+        send.free()
+        recv.free()
+        comm.destroy()
+        out_q.put((rank, res))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
 def stall_rank(rank, n, port, env, call_allreduce, out_q):
     """Timeout test: rank 0 calls all-reduce, the other ranks never do."""
     try:

@@ -105,6 +105,14 @@ def test_allreduce_fp32_sum(dev, n, algo):
 
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+def test_allreduce_8_ranks(dev, algo):
+    # the 8-GPU node's rank count, all on GPU 0: every pair of the mesh is exercised
+    cases = [_case(count=(1 << 20) + 5, algo=algo, seed=8), _case(dtype="bf16", count=(1 << 19) + 3, algo=algo,
+                                                                    inplace=True, seed=9)]
+    _run_allreduce(8, cases, env={"MINI_NCCL_CHANNELS": "16"})
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
 def test_allreduce_dtypes_ops(dev, algo):
     cases = [_case(dtype=d, op=o, count=50000 + 7 * i, algo=algo, seed=100 + i, special=o in ("max", "min"))
              for i, (d, o) in enumerate((d, o) for d in DTYPES for o in OPS)]
@@ -159,3 +167,13 @@ def test_allreduce_hip_graph_capture_and_replay(dev, algo):
         assert out[r]["capture_rc"] == [0]
         assert out[r]["bad"] == [0, 0, 0, 0]
         assert out[r]["eager_rc"] == 0 and out[r]["eager_bad"] == 0
+
+
+def test_link_probe_then_allreduce(dev):
+    port = GW.free_port()
+    out = GW.run_ranks(GW.probe_rank, 3, lambda r: (r, 3, port, {"MINI_NCCL_TIMEOUT_MS": "20000"}), 180)
+    assert sorted(out) == [0, 1, 2], out
+    for r in range(3):
+        assert "error" not in out[r], out[r]["error"]
+        assert out[r]["next"] > 0 and out[r]["mesh"] > 0
+        assert out[r]["rc"] == 0 and out[r]["exact"]
