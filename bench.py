@@ -346,4 +346,13 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as e:  # still one JSON line from rank 0, so the failure is on record
+        import traceback
+        traceback.print_exc()
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "GB/s",
+                              "n_gpus": int(os.environ.get("WORLD_SIZE", "1")), "higher_is_better": True,
+                              "error": f"{type(e).__name__}: {e}"[:500]}), flush=True)
+        sys.exit(1)

@@ -304,7 +304,10 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     p.host_abort = d_ctl_ + 1;
     p.timeout_ticks = (uint64_t)(cfg_.timeout_ms * 1e5);  // s_memrealtime runs at 100 MHz
     p.sys_fence = cfg_.sys_fence;
-    const bool vec = (((uintptr_t)send | (uintptr_t)recv) % 16 == 0) && (chunk_bytes % 16 == 0);
+    // 16-byte vector path whenever every message's local base is dword-aligned (vectors may
+    // straddle 16-byte boundaries on the local side; each message's last len % 16 bytes go
+    // element by element); element-wise path otherwise (2-byte types with odd chunks)
+    const bool vec = (((uintptr_t)send | (uintptr_t)recv) % 4 == 0) && (chunk_bytes % 4 == 0);
     hipError_t e = algo_ == 1 ? launch_direct(dtype, op, vec, cfg_.channels, cfg_.threads, p, stream)
                               : launch_ring(dtype, op, vec, cfg_.channels, cfg_.threads, p, stream);
     hip_check(e, "kernel launch");

@@ -209,6 +209,13 @@ __device__ __forceinline__ void vec_one(const char* lsrc, char* ldst, rsrc_t in,
 }
 
 template <typename T, int OPC, int KIND>
+__device__ __forceinline__ void move_scalar(const char* __restrict__ lsrc, char* __restrict__ ldst, rsrc_t in,
+                                            rsrc_t out, uint32_t nbytes, int lane, uint32_t off0);
+
+// 16-byte vectors over the message, then its last (nbytes % 16) bytes element by element.
+// The local side (send / recv) may be element- but not 16-byte-aligned (4-byte-aligned
+// dwordx4 accesses are valid on gfx950); the slot side is always 16-byte-aligned.
+template <typename T, int OPC, int KIND>
 __device__ __forceinline__ void move_vec(const char* __restrict__ lsrc, char* __restrict__ ldst, rsrc_t in,
                                          rsrc_t out, uint32_t nbytes, int lane) {
   constexpr int B = KindBits<KIND>::v;
@@ -234,15 +241,17 @@ __device__ __forceinline__ void move_vec(const char* __restrict__ lsrc, char* __
     }
   }
   for (uint32_t i = b + (uint32_t)lane; i < nvec; i += 64) vec_one<T, OPC, KIND>(lsrc, ldst, in, out, i);
+  if (nbytes & 15u) move_scalar<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, lane, nvec * 16);
 }
 
+// elements [off0 / sizeof(T), nbytes / sizeof(T)) of the message, one per lane
 template <typename T, int OPC, int KIND>
 __device__ __forceinline__ void move_scalar(const char* __restrict__ lsrc, char* __restrict__ ldst, rsrc_t in,
-                                            rsrc_t out, uint32_t nbytes, int lane) {
+                                            rsrc_t out, uint32_t nbytes, int lane, uint32_t off0) {
   constexpr int B = KindBits<KIND>::v;
   typedef typename Scal<sizeof(T)>::U U;
   const uint32_t ne = nbytes / sizeof(T);
-  for (uint32_t i = lane; i < ne; i += 64) {
+  for (uint32_t i = off0 / sizeof(T) + lane; i < ne; i += 64) {
     U l = 0, x = 0, v;
     if (B & kHasLocal) l = reinterpret_cast<const U*>(lsrc)[i];
     if (B & kHasIn) x = Scal<sizeof(T)>::ld(in, i * (uint32_t)sizeof(T));
@@ -257,7 +266,7 @@ __device__ __forceinline__ void move_scalar(const char* __restrict__ lsrc, char*
 template <typename T, int OPC, bool VEC, int KIND>
 __device__ __forceinline__ void move(const char* lsrc, char* ldst, rsrc_t in, rsrc_t out, uint32_t nbytes, int lane) {
   if (VEC) move_vec<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, lane);
-  else move_scalar<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, lane);
+  else move_scalar<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, lane, 0);
 }
 
 __device__ __forceinline__ void abort_peers(const CollParams& p, int C, int a, int b) {
@@ -342,6 +351,30 @@ __global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
 }
 
 // ---------------------------------------------------------------- direct kernel
+// element-wise fold for elements [off0 / sizeof(T), nbytes / sizeof(T)) of the slice
+template <typename T, int OPC>
+__device__ __forceinline__ void fold_scalar(const CollParams& p, const char* lsrc, char* ldst, const u64* rx0,
+                                            const u64* tx1, uint32_t nbytes, int w, int C, int lane, uint32_t off0) {
+  const int n = p.n, r = p.rank, K = p.nslots;
+  typedef typename Scal<sizeof(T)>::U Us;
+  const uint32_t ne = nbytes / sizeof(T);
+  for (uint32_t i = off0 / sizeof(T) + lane; i < ne; i += 64) {
+    T acc = reinterpret_cast<const T*>(lsrc)[i];
+    for (int k = 1; k < n; ++k) {
+      const int q = direct_peer(n, r, k);
+      const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q]), nbytes);
+      const T x = __builtin_bit_cast(T, Scal<sizeof(T)>::ld(in, i * (uint32_t)sizeof(T)));
+      acc = Op<T, OPC>::f(x, acc);
+    }
+    reinterpret_cast<T*>(ldst)[i] = acc;
+    for (int k = 1; k < n; ++k) {
+      const int d = direct_peer(n, r, k);
+      const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slice_bytes, r, w, tx1[d]), nbytes);
+      Scal<sizeof(T)>::st(out, i * (uint32_t)sizeof(T), __builtin_bit_cast(Us, acc));
+    }
+  }
+}
+
 // Fold of the n-1 arriving slices of this rank's own chunk, software-pipelined by one
 // peer so two slot loads per vector are in flight; acc = op(x_q, acc) in ring order.
 // rx0[q]: sequence number of q's raw message for this slice; tx1[d]: of my result message to d
@@ -393,24 +426,9 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
           if (live[u]) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
       }
     }
+    if (nbytes & 15u) fold_scalar<T, OPC>(p, lsrc, ldst, rx0, tx1, nbytes, w, C, lane, nvec * 16);
   } else {
-    typedef typename Scal<sizeof(T)>::U Us;
-    const uint32_t ne = nbytes / sizeof(T);
-    for (uint32_t i = lane; i < ne; i += 64) {
-      T acc = reinterpret_cast<const T*>(lsrc)[i];
-      for (int k = 1; k < n; ++k) {
-        const int q = direct_peer(n, r, k);
-        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q]), nbytes);
-        const T x = __builtin_bit_cast(T, Scal<sizeof(T)>::ld(in, i * (uint32_t)sizeof(T)));
-        acc = Op<T, OPC>::f(x, acc);
-      }
-      reinterpret_cast<T*>(ldst)[i] = acc;
-      for (int k = 1; k < n; ++k) {
-        const int d = direct_peer(n, r, k);
-        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slice_bytes, r, w, tx1[d]), nbytes);
-        Scal<sizeof(T)>::st(out, i * (uint32_t)sizeof(T), __builtin_bit_cast(Us, acc));
-      }
-    }
+    fold_scalar<T, OPC>(p, lsrc, ldst, rx0, tx1, nbytes, w, C, lane, 0);
   }
 }
 
@@ -653,20 +671,24 @@ static hipError_t direct_for_t(int op, bool vec, int C, int nt, const CollParams
 
 template <typename T>
 static hipError_t local_for_t(int op, void* out, const void* a, const void* b, u64 count, hipStream_t st) {
-  const bool vec = (((uintptr_t)out | (uintptr_t)a | (uintptr_t)b) % 16 == 0) && ((count * sizeof(T)) % 16 == 0);
-  const u64 nvec = count * sizeof(T) / 16;
+  // 16-byte vectors over the body whenever the three buffers are dword-aligned (4-byte-aligned
+  // dwordx4 accesses are valid on gfx950), then the last (bytes % 16) bytes element-wise
+  const bool vec = ((uintptr_t)out | (uintptr_t)a | (uintptr_t)b) % 4 == 0;
+  const u64 nvec = vec ? count * sizeof(T) / 16 : 0;
+  const u64 done = nvec * 16 / sizeof(T);
   const u64 kMaxExactBlocks = (1ull << 31) / 64;  // keep the exact grid under 2^31 threads
 #define LOCAL_CASE(OPC)                                                                                         \
   case OPC:                                                                                                     \
-    if (vec && (nvec + 63) / 64 <= kMaxExactBlocks)                                                             \
+    if (nvec && (nvec + 63) / 64 <= kMaxExactBlocks)                                                            \
       hipLaunchKernelGGL((local_reduce_vec<T, OPC>), dim3((unsigned)((nvec + 63) / 64)), dim3(64), 0, st,      \
                          (char*)out, (const char*)a, (const char*)b, nvec);                                     \
-    else if (vec)                                                                                               \
+    else if (nvec)                                                                                              \
       hipLaunchKernelGGL((local_reduce_vec_gs<T, OPC>), dim3(16384), dim3(256), 0, st, (char*)out,             \
                          (const char*)a, (const char*)b, nvec);                                                 \
-    else                                                                                                        \
-      hipLaunchKernelGGL((local_reduce_scalar<T, OPC>), dim3((unsigned)std::min<u64>((count + 255) / 256, 16384)), \
-                         dim3(256), 0, st, (T*)out, (const T*)a, (const T*)b, count);                           \
+    if (count > done)                                                                                           \
+      hipLaunchKernelGGL((local_reduce_scalar<T, OPC>),                                                         \
+                         dim3((unsigned)std::min<u64>((count - done + 255) / 256, 16384)), dim3(256), 0, st,    \
+                         (T*)out + done, (const T*)a + done, (const T*)b + done, count - done);                 \
     break;
   switch (op) {
     LOCAL_CASE(kSum) LOCAL_CASE(kProd) LOCAL_CASE(kMax) LOCAL_CASE(kMin)

@@ -33,7 +33,7 @@ def dev(nccl_lib, oracle_lib):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("op", OPS)
-@pytest.mark.parametrize("count,offset", [(1 << 20, 0), (100003, 0), (4099, 4), (17, 2)])
+@pytest.mark.parametrize("count,offset", [(1 << 20, 0), (100003, 0), (4099, 4), (17, 2), (65539, 1), (1 << 16, 3)])
 def test_local_reduce_parity(dev, dtype, op, count, offset):
     import mini_nccl as M
     code, npd = O.DTYPES[dtype]
@@ -125,9 +125,12 @@ def test_allreduce_small_slices_many_messages(dev):
     _run_allreduce(4, cases, env={"MINI_NCCL_SLICE_SIZE": "1024", "MINI_NCCL_CHANNELS": "4"})
 
 
-def test_allreduce_misaligned_scalar_path(dev):
-    cases = [_case(count=40001, algo=a, offset=4, seed=5) for a in (0, 1)]
-    _run_allreduce(2, cases)
+def test_allreduce_misaligned_buffers(dev):
+    # dword-aligned but not 16-byte-aligned buffers (vector path with straddling vectors)
+    # and 2-byte-aligned halves with odd chunks (element path)
+    cases = [_case(count=40001, algo=a, offset=o, seed=5) for a in (0, 1) for o in (4, 8, 12)]
+    cases += [_case(dtype="bf16", count=30001, algo=a, offset=2, seed=6) for a in (0, 1)]
+    _run_allreduce(3, cases)
 
 
 def test_allreduce_async_mode(dev):
