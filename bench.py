@@ -105,6 +105,81 @@ def cpu_baseline(budget_s=10.0):
     }
 
 
+# ------------------------------------------------------------------ N > 1 configuration sweeps
+# (workgroups, threads, slice, algo, sys_fence) points timed on a 256 MiB buffer, and the
+# BASELINE.json configs[3] (C4) grid: ring, 4 GiB fp32, SLICE x WINDOW.  Each point builds its
+# own communicator (the knobs are read at ncclCommInitRank, as the reference's Config).
+SWEEP_POINTS = [
+    # (MINI_NCCL_CHANNELS, MINI_NCCL_THREADS, MINI_NCCL_SLICE_SIZE, algo, MINI_NCCL_SYS_FENCE)
+    (16, 256, 131072, "direct", 1), (32, 256, 131072, "direct", 1), (64, 256, 131072, "direct", 1),
+    (128, 256, 131072, "direct", 1), (64, 256, 524288, "direct", 1), (128, 64, 524288, "direct", 1),
+    (64, 256, 131072, "direct", 0),
+    (16, 256, 131072, "ring", 1), (64, 256, 131072, "ring", 1), (64, 256, 524288, "ring", 1),
+    (128, 64, 524288, "ring", 1), (64, 256, 131072, "ring", 0),
+]
+C4_SLICES = [65536, 131072, 262144, 1048576]
+C4_WINDOWS = [16, 32, 64]
+
+
+def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_ranks):
+    """one communicator with `env` knobs; returns algbw GB/s (max time over ranks) and check"""
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    comm = None
+    try:
+        comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
+        comm.set_algo(M.ALGO_DIRECT if algo == "direct" else M.ALGO_RING)
+        st = torch.cuda.Stream(device=dev)
+        send = torch.ones(count, device=dev, dtype=torch.float32)
+        recv = torch.empty(count, device=dev, dtype=torch.float32)
+
+        def call():
+            rc = comm.all_reduce(send.data_ptr(), recv.data_ptr(), count, M.ncclFloat, M.ncclSum, st.cuda_stream)
+            if rc != 0:
+                raise M.NcclError(rc, "ncclAllReduce")
+
+        call()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            call()
+        torch.cuda.synchronize()
+        dt = max_over_ranks(time.perf_counter() - t0)
+        ok = comm.async_error() == 0 and bool((recv == float(n)).all().item())
+        ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
+        return {"GBps": round(count * 4 / (dt / reps) / 1e9, 2), "ok": ok}
+    except Exception as e:
+        return {"error": str(e)[:120]}
+    finally:
+        if comm is not None:
+            comm.destroy()
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        torch.cuda.empty_cache()
+
+
+def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
+    out = {"buffer": "256 MiB fp32", "points": []}
+    for ch, thr, sl, algo, fence in SWEEP_POINTS:
+        env = {"MINI_NCCL_CHANNELS": ch, "MINI_NCCL_THREADS": thr, "MINI_NCCL_SLICE_SIZE": sl,
+               "MINI_NCCL_SYS_FENCE": fence}
+        r = sweep_point(M, torch, dist, dev, n, rank, env, algo, 64 << 20, 5, max_over_ranks)
+        out["points"].append({"algo": algo, "channels": ch, "threads": thr, "slice": sl, "sys_fence": fence, **r})
+    if with_c4:  # BASELINE.json configs[3]: ring, 4 GiB fp32, SLICE x WINDOW
+        c4 = []
+        for w in C4_WINDOWS:
+            for sl in C4_SLICES:
+                env = {"MINI_NCCL_WINDOW_SIZE": w, "MINI_NCCL_SLICE_SIZE": sl}
+                r = sweep_point(M, torch, dist, dev, n, rank, env, "ring", 1 << 30, 3, max_over_ranks)
+                c4.append({"window": w, "slice": sl, **r})
+        out["c4_ring_4GiB"] = c4
+    return out
+
+
 # ------------------------------------------------------------------ helpers
 def reduce_max(dist, x):
     """max over ranks of a host scalar through the harness's (gloo) process group"""
@@ -139,6 +214,7 @@ def main():
                     help="auto = the library default (ring at 2 ranks, direct from 3: same bits, every link)")
     ap.add_argument("--no-alt", action="store_true", help="N>1: skip the second schedule and the RCCL reference")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true", help="N>1: skip the configuration sweeps")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on GPU 0 (as the reference's perf_test)")
     args = ap.parse_args()
@@ -338,10 +414,17 @@ def main():
         except Exception as e:
             result["rccl_reference"] = {"error": str(e)[:200]}
     result["cpu_baseline"] = cpu
+    if n > 1:
+        comm.destroy()
+        del send, recv
+        torch.cuda.empty_cache()
+        if not args.no_sweep and args.dtype == "f32":
+            t_sw = time.time()
+            result["sweep"] = run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4=(n == 8))
+            result["sweep"]["wall_s"] = round(time.time() - t_sw, 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if n > 1:
-        comm.destroy()
         dist.destroy_process_group()
 
 

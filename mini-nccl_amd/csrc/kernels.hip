@@ -419,7 +419,7 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
       for (int u = 0; u < U; ++u)
         if (live[u]) st_g16(ldst + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
       for (int k = 1; k < n; ++k) {
-        const int d = direct_peer(n, r, k);
+        const int d = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));  // staggered like phase A
         const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slice_bytes, r, w, tx1[d]), nbytes);
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -466,9 +466,11 @@ __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
     __builtin_amdgcn_wave_barrier();
 
     // Phase A: push my raw slice of chunk d to rank d, for every peer d; one drain for all
-    // n-1 pushes, then the n-1 READY flags
+    // n-1 pushes, then the n-1 READY flags.  Pipeline w starts at peer (w mod n-1): the
+    // pipelines of a rank spread over all n-1 xGMI links instead of marching through them
+    // one link at a time (the push order does not touch the fold order).
     for (int k = 1; k < n; ++k) {
-      const int d = direct_peer(n, r, k);
+      const int d = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));
       const u64 seq0 = tx[d] + itoff;
       if (seq0 + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, d, w), seq0 + 1 - K, ctl, lane)) goto aborted;
       if (len) {

@@ -119,6 +119,13 @@ def test_allreduce_dtypes_ops(dev, algo):
     _run_allreduce(3, cases)
 
 
+def test_allreduce_c2_full_size(dev):
+    # BASELINE.json configs[1] (C2): 2 ranks, 256 MiB fp32, MINI_NCCL_SLICE_SIZE = 128 KiB,
+    # seeded uniform inputs, bit-exact against the oracle at full size
+    cases = [_case(count=64 << 20, algo=0, seed=1234)]
+    _run_allreduce(2, cases, env={"MINI_NCCL_SLICE_SIZE": "131072"}, timeout=600)
+
+
 def test_allreduce_small_slices_many_messages(dev):
     # 1 KiB slices, 4 channels: thousands of flag hand-offs per call, both schedules
     cases = [_case(count=(1 << 19) + 5, algo=a, calls=2, seed=77) for a in (0, 1)]
