@@ -207,6 +207,17 @@ ncclResult_t Comm::check_status() {
     fprintf(stderr, "[Mini-NCCL] rank %d: all-reduce %s (status 0x%x); communicator is no longer usable\n", rank_,
             (st & kStatusTimeout) ? "timed out (watchdog)" : (st & kStatusHostAbort) ? "aborted by host" : "aborted by a peer",
             st);
+    if (st & kStatusTimeout) {
+      // which mailbox word the first timed-out wait was stuck on (kernels.hip record_timeout)
+      const volatile uint64_t* diag = reinterpret_cast<const volatile uint64_t*>(h_ctl_ + 4);
+      const uint64_t word = diag[0], line = word / kFlagStride;
+      const int P = wave_channels(), n = nranks_;
+      const bool ready = line < (uint64_t)n * P;
+      const uint64_t idx = ready ? line : line - (uint64_t)n * P;
+      fprintf(stderr, "[Mini-NCCL] rank %d: stuck on %s word of peer %llu, pipeline %llu: waiting for >= %llu, saw %llu\n",
+              rank_, ready ? "READY" : "CREDIT", (unsigned long long)(idx / P), (unsigned long long)(idx % P),
+              (unsigned long long)diag[1], (unsigned long long)diag[2]);
+    }
   }
   return sticky_;
 }

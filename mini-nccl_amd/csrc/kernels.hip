@@ -144,7 +144,19 @@ struct Ctl {
   const uint32_t* host_abort;
   const u64* my_abort;
   uint64_t timeout_ticks;
+  const u64* mbox;  // this rank's mailbox base (for the timeout diagnostic)
 };
+
+// a timed-out wait: which mailbox word, the target and the last value seen (host-mapped words
+// 4..9 of the control page; plain system-scope stores, no PCIe atomics; only the first wave to
+// time out -- the others see a non-zero status -- normally writes them)
+__device__ __forceinline__ void record_timeout(const Ctl& c, const u64* flag, u64 target, u64 seen) {
+  if (ld_sys32(c.status) != 0) return;
+  u64* diag = reinterpret_cast<u64*>(c.status + 4);
+  __hip_atomic_store(diag + 0, (u64)(flag - c.mbox), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(diag + 1, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(diag + 2, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // lane-0 spin until *flag >= target; false on timeout / abort (status already set)
 __device__ __noinline__ bool wait_ge(const u64* flag, u64 target, const Ctl& c) {
@@ -157,7 +169,11 @@ __device__ __noinline__ bool wait_ge(const u64* flag, u64 target, const Ctl& c) 
       if (ld_sys(c.my_abort) != 0) { st_sys32(c.status, kStatusRemoteAbort); return false; }
       if (ld_sys32(c.host_abort) != 0) { st_sys32(c.status, kStatusHostAbort); return false; }
       if (ld_sys32(c.status) != 0) return false;  // a sibling workgroup gave up
-      if (__builtin_amdgcn_s_memrealtime() - t0 > c.timeout_ticks) { st_sys32(c.status, kStatusTimeout); return false; }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > c.timeout_ticks) {
+        record_timeout(c, flag, target, ld_sys(flag));
+        st_sys32(c.status, kStatusTimeout);
+        return false;
+      }
     }
   }
 }
@@ -295,7 +311,7 @@ __global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
   const int lane = id.lane, w = id.w, C = id.C;
   const int n = p.n, r = p.rank, K = p.nslots;
   const int prev = mod_n(r - 1, n), next = mod_n(r + 1, n);
-  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks};
+  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox};
   // per-pair message counters: the FIFO to `next` and the FIFO from `prev` on this channel
   u64* tx_ctr = p.tx_seq + (u64)next * C + w;
   u64* rx_ctr = p.rx_seq + (u64)prev * C + w;
@@ -446,7 +462,7 @@ __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
   u64* rx = s_rx[wv];
   u64* rx0 = s_rx0[wv];
   u64* tx1 = s_tx1[wv];
-  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks};
+  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox};
   const int mpi = direct_msgs_per_iter();
   if (lane < n) {
     tx[lane] = p.tx_seq[(u64)lane * C + w];

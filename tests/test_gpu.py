@@ -71,7 +71,7 @@ def test_local_reduce_in_place_large(dev):
 
 def _run_allreduce(n, cases, env=None, timeout=300):
     port = GW.free_port()
-    e = {"MINI_NCCL_TIMEOUT_MS": "20000"}
+    e = {"MINI_NCCL_TIMEOUT_MS": "30000"}
     e.update(env or {})
     out = GW.run_ranks(GW.allreduce_rank, n, lambda r: (r, n, port, cases, e), timeout)
     assert len(out) == n, f"only ranks {sorted(out)} reported (timeout?)"
@@ -109,7 +109,9 @@ def test_allreduce_8_ranks(dev, algo):
     # the 8-GPU node's rank count, all on GPU 0: every pair of the mesh is exercised
     cases = [_case(count=(1 << 20) + 5, algo=algo, seed=8), _case(dtype="bf16", count=(1 << 19) + 3, algo=algo,
                                                                     inplace=True, seed=9)]
-    _run_allreduce(8, cases, env={"MINI_NCCL_CHANNELS": "16"})
+    # 8 processes time-share one GPU here: fewer workgroups and a longer watchdog than the
+    # defaults (the 8-GPU node gives each rank its own GPU)
+    _run_allreduce(8, cases, env={"MINI_NCCL_CHANNELS": "8", "MINI_NCCL_TIMEOUT_MS": "60000"}, timeout=400)
 
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
