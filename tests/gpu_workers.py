@@ -170,6 +170,57 @@ def probe_rank(rank, n, port, env, out_q):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def init_rank(rank, n, port, env, out_q):
+    """ncclCommInitRank with per-rank environment (env[rank]); report the result code."""
+    try:
+        os.environ.update(env.get(rank, {}))
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import ctypes
+        import hip_rt
+        import mini_nccl as M
+        hip_rt.set_device(0)
+        h = ctypes.c_void_p()
+        rc = M.load().ncclCommInitRank(ctypes.byref(h), n, rank, b"127.0.0.1")
+        if rc == 0:
+            M.load().ncclCommDestroy(h)
+        out_q.put((rank, {"rc": rc}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
+def huge_rank(rank, n, port, env, count, out_q):
+    """64-bit element counts (the reference narrowed count to int, mini_nccl.h:113): bf16
+    all-ones in place -> body == n, tail == 1 (size-independent known answer)."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        hip_rt.set_device(0)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        buf = hip_rt.DeviceBuffer(count * 2)
+        chunk = 1 << 26
+        ones = np.full(chunk, 0x3F80, np.uint16)  # bf16 1.0
+        for off in range(0, count, chunk):
+            m = min(chunk, count - off)
+            buf.upload(ones[:m], off * 2)
+        rc = comm.all_reduce(buf.ptr, buf.ptr, count, M.ncclBfloat16, M.ncclSum, 0)
+        hip_rt.sync()
+        body = (count // n) * n
+        want = {2: 0x4000, 4: 0x4080}[n]
+        bad = 0
+        for off in range(0, count, chunk):
+            m = min(chunk, count - off)
+            got = buf.download(np.uint16, m, off * 2)
+            idx = np.arange(off, off + m)
+            bad += int((got != np.where(idx < body, want, 0x3F80)).sum())
+        buf.free()
+        comm.destroy()
+        out_q.put((rank, {"rc": rc, "bad": bad}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
 def stall_rank(rank, n, port, env, call_allreduce, out_q):
     """Timeout test: rank 0 calls all-reduce, the other ranks never do."""
     try:

@@ -189,3 +189,30 @@ def test_link_probe_then_allreduce(dev):
         assert "error" not in out[r], out[r]["error"]
         assert out[r]["next"] > 0 and out[r]["mesh"] > 0
         assert out[r]["rc"] == 0 and out[r]["exact"]
+
+
+def test_single_rank_is_copy_only(dev):
+    # nRanks == 1: the reference returns after the send->recv copy (mini_nccl.cu:66)
+    cases = [_case(count=100001, seed=4), _case(count=4097, inplace=True, seed=5),
+             _case(dtype="f64", op="max", count=3001, seed=6)]
+    _run_allreduce(1, cases)
+
+
+def test_mismatched_config_is_invalid_usage(dev):
+    import mini_nccl as M
+    port = GW.free_port()
+    env = {0: {"MINI_NCCL_SLICE_SIZE": "131072"}, 1: {"MINI_NCCL_SLICE_SIZE": "65536"}}
+    out = GW.run_ranks(GW.init_rank, 2, lambda r: (r, 2, port, env), 120)
+    assert sorted(out) == [0, 1], out
+    assert out[0]["rc"] == M.ncclInvalidUsage and out[1]["rc"] == M.ncclInvalidUsage
+
+
+def test_count_beyond_int32(dev):
+    # 2^31 + 7 bf16 elements per rank (4 GiB): 64-bit counts end to end
+    port = GW.free_port()
+    count = (1 << 31) + 7
+    out = GW.run_ranks(GW.huge_rank, 2, lambda r: (r, 2, port, {"MINI_NCCL_TIMEOUT_MS": "60000"}, count), 600)
+    assert sorted(out) == [0, 1], out
+    for r in range(2):
+        assert "error" not in out[r], out[r]["error"]
+        assert out[r]["rc"] == 0 and out[r]["bad"] == 0, out[r]
