@@ -1,16 +1,18 @@
 // perf_test -- the reference's measurement harness (tests/perf_test.cpp:34-158) for the
 // MI355X build, written against the same C ABI (include/mini_nccl_api.h).
 //
-//   perf_test <rank> <n_ranks> [master_ip] [--mode device|staged] [--sizes MiB,MiB,...]
+//   perf_test <rank> <n_ranks> [master_ip] [--mode device|host|staged] [--sizes MiB,MiB,...]
 //
 // Same protocol as the reference: sizes 1/16/64/128 MiB fp32, every rank sends 1.0, 5
 // warm-up and 20 timed all-reduces between CLOCK_MONOTONIC reads, an AVX2 compare scan
 // that every element equals nRanks, and the algbw / busbw table
 // (algbw = bytes / time, busbw = algbw * 2(n-1)/n; perf_test.cpp:140-143).
 //   --mode device  (default) buffers resident in HBM: the headline measurement;
-//   --mode staged  the reference's host-resident buffers (it used cudaHostAlloc,
-//                  perf_test.cpp:78-79): pinned host -> H2D -> all-reduce -> D2H per call,
-//                  i.e. the end-to-end rate including PCIe.
+//   --mode host    the reference's own usage: pinned host buffers (cudaHostAlloc,
+//                  perf_test.cpp:78-79) handed straight to ncclAllReduce; the kernel reads
+//                  and writes them through their device mapping, i.e. the end-to-end rate
+//                  including PCIe (MINI_NCCL_STAGE_HOST=1: staged through HBM instead);
+//   --mode staged  pinned host -> explicit H2D -> all-reduce -> D2H per call.
 // Device: rank % device_count (the reference pinned every rank to GPU 0, :46;
 // MINI_NCCL_PERF_DEVICE overrides).
 #include <hip/hip_runtime.h>
@@ -66,7 +68,7 @@ static long first_mismatch(const float* p, size_t n, float expected) {
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "Usage: %s <rank> <n_ranks> [master_ip] [--mode device|staged] [--sizes 1,16,64,128]\n", argv[0]);
+    fprintf(stderr, "Usage: %s <rank> <n_ranks> [master_ip] [--mode device|host|staged] [--sizes 1,16,64,128]\n", argv[0]);
     return 1;
   }
   const int rank = atoi(argv[1]);
@@ -97,7 +99,7 @@ int main(int argc, char** argv) {
 
   if (rank == 0) {
     printf("\n=== Mini-NCCL (MI355X) Performance Benchmark, %d ranks, %s buffers ===\n", nranks,
-           mode == "device" ? "HBM-resident" : "host-staged (H2D + all-reduce + D2H)");
+           mode == "device" ? "HBM-resident" : mode == "host" ? "pinned host buffers passed to ncclAllReduce" : "host-staged (H2D + all-reduce + D2H)");
     printf("%15s %15s %15s %15s\n", "Size(B)", "Time(us)", "AlgBW(GB/s)", "BusBW(GB/s)");
   }
   int failures = 0;
@@ -114,7 +116,8 @@ int main(int argc, char** argv) {
 
     auto one = [&]() {
       if (mode == "staged") HIP_OK(hipMemcpyAsync(d_send, h_send, bytes, hipMemcpyHostToDevice, stream));
-      NCCL_OK(ncclAllReduce(d_send, d_recv, count, ncclFloat, ncclSum, comm, stream));
+      if (mode == "host") NCCL_OK(ncclAllReduce(h_send, h_recv, count, ncclFloat, ncclSum, comm, stream));
+      else NCCL_OK(ncclAllReduce(d_send, d_recv, count, ncclFloat, ncclSum, comm, stream));
       if (mode == "staged") HIP_OK(hipMemcpyAsync(h_recv, d_recv, bytes, hipMemcpyDeviceToHost, stream));
     };
     for (int i = 0; i < warmup; ++i) one();
@@ -123,7 +126,7 @@ int main(int argc, char** argv) {
     for (int i = 0; i < iters; ++i) one();
     HIP_OK(hipStreamSynchronize(stream));
     const double t1 = now_us();
-    if (mode != "staged") HIP_OK(hipMemcpy(h_recv, d_recv, bytes, hipMemcpyDeviceToHost));
+    if (mode == "device") HIP_OK(hipMemcpy(h_recv, d_recv, bytes, hipMemcpyDeviceToHost));
 
     // every element of the n * (count / n) body is the sum; the count % n tail keeps this
     // rank's own input (1.0): the reference never reduces it (mini_nccl.cu:69), so its own

@@ -190,6 +190,9 @@ void Comm::release() {
   if (mbox_) hipFree(mbox_);
   if (pair_seq_) hipFree(pair_seq_);
   if (h_ctl_) hipHostFree(h_ctl_);
+  if (stage_) hipFree(stage_);
+  stage_ = nullptr;
+  stage_bytes_ = 0;
   if (done_) hipEventDestroy(done_);
   scratch_ = nullptr;
   mbox_ = nullptr;
@@ -255,6 +258,73 @@ ncclResult_t Comm::wait_for(hipStream_t stream) {
   return check_status();
 }
 
+// Which memory the kernel can address for a user buffer (see allreduce).
+Comm::Reach Comm::reach(const void* p, const void** kernel_ptr) const {
+  hipPointerAttribute_t a;
+  memset(&a, 0, sizeof a);
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return Reach::kStaged;  // not known to HIP: pageable host memory
+  }
+  if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged) return Reach::kDevice;
+  if (a.type == hipMemoryTypeHost && a.devicePointer && !cfg_.stage_host) {
+    // device address of p itself (devicePointer / hostPointer may name the allocation base)
+    const char* hp = (const char*)(a.hostPointer ? a.hostPointer : p);
+    *kernel_ptr = (const char*)a.devicePointer + ((const char*)p - hp);
+    return Reach::kMapped;
+  }
+  return Reach::kStaged;
+}
+
+void Comm::ensure_stage(size_t bytes) {
+  if (stage_bytes_ >= bytes) return;
+  if (stage_) {
+    hip_check(hipDeviceSynchronize(), "stage regrow sync");  // earlier calls may still use it
+    hip_check(hipFree(stage_), "free stage");
+    stage_ = nullptr;
+    stage_bytes_ = 0;
+  }
+  const size_t want = (bytes + ((size_t)1 << 20) - 1) & ~(((size_t)1 << 20) - 1);
+  hip_check(hipMalloc((void**)&stage_, want), "alloc stage");
+  stage_bytes_ = want;
+}
+
+void Comm::launch_ring_or_direct(const void* send, void* recv, size_t chunk_bytes, int dtype, int op,
+                                 hipStream_t stream) {
+  const int n = nranks_;
+  CollParams p;
+  memset(&p, 0, sizeof p);
+  p.send = (const char*)send;
+  p.recv = (char*)recv;
+  p.chunk_bytes = chunk_bytes;
+  p.slice_bytes = wave_slice();
+  p.nslices = (chunk_bytes + p.slice_bytes - 1) / p.slice_bytes;
+  const int C = wave_channels();
+  p.iters = (uint32_t)((p.nslices + (uint64_t)C - 1) / (uint64_t)C);
+  p.n = n;
+  p.rank = rank_;
+  p.nslots = cfg_.slots;
+  p.scratch = scratch_;
+  p.mbox = mbox_;
+  p.tx_seq = pair_seq_;
+  p.rx_seq = pair_seq_ + (size_t)n * C;
+  for (int q = 0; q < n; ++q) {
+    p.peer_scratch[q] = peer_scratch_[(size_t)q];
+    p.peer_mbox[q] = peer_mbox_[(size_t)q];
+  }
+  p.status = d_ctl_;
+  p.host_abort = d_ctl_ + 1;
+  p.timeout_ticks = (uint64_t)(cfg_.timeout_ms * 1e5);  // s_memrealtime runs at 100 MHz
+  p.sys_fence = cfg_.sys_fence;
+  // 16-byte vector path whenever every message's local base is dword-aligned (vectors may
+  // straddle 16-byte boundaries on the local side; each message's last len % 16 bytes go
+  // element by element); element-wise path otherwise (2-byte types with odd chunks)
+  const bool vec = (((uintptr_t)send | (uintptr_t)recv) % 4 == 0) && (chunk_bytes % 4 == 0);
+  hipError_t e = algo_ == 1 ? launch_direct(dtype, op, vec, cfg_.channels, cfg_.threads, p, stream)
+                            : launch_ring(dtype, op, vec, cfg_.channels, cfg_.threads, p, stream);
+  hip_check(e, "kernel launch");
+}
+
 ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t stream) {
   if (sticky_ != ncclSuccess) return sticky_;
   if (check_status() != ncclSuccess) return sticky_;
@@ -281,47 +351,39 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
   const size_t chunk_bytes = chunk * (size_t)esz;
   if (n == 1 || chunk == 0) {
     // nRanks == 1 returns after the copy (mini_nccl.cu:66); chunk == 0 moves no slice
-    if (send != recv) hip_check(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, stream), "copy");
+    if (send != recv) hip_check(hipMemcpyAsync(recv, send, bytes, hipMemcpyDefault, stream), "copy");
   } else {
+    // Where the kernel reads and writes: device memory as is; pinned / registered host
+    // memory through its device mapping (the kernel then streams it over PCIe itself,
+    // pipelined slice by slice -- what the reference's kernels did with its
+    // cudaHostAlloc'd perf_test buffers, perf_test.cpp:78-79); pageable host memory
+    // through a device staging copy.  Every rank launches the same kernel either way.
+    const void* ksend = send;
+    void* krecv = recv;
+    const Reach rs = reach(send, &ksend), rr = reach(recv, (const void**)&krecv);
+    if (rs == Reach::kStaged || rr == Reach::kStaged) {
+      if (cap != hipStreamCaptureStatusNone) {
+        fprintf(stderr, "[Mini-NCCL] pageable host buffers cannot be captured into a HIP graph\n");
+        if (cur_dev != device_) hipSetDevice(cur_dev);
+        return ncclInvalidUsage;
+      }
+      ensure_stage(bytes);
+      if (rs == Reach::kStaged) {
+        hip_check(hipMemcpyAsync(stage_, send, bytes, hipMemcpyDefault, stream), "stage in");
+        ksend = stage_;
+      }
+      if (rr == Reach::kStaged) krecv = stage_;  // also in place when send is staged too
+    }
     // elements past n*chunk keep this rank's own input (the reference copies the whole
     // buffer and never touches the tail, api.cpp:173-175 + mini_nccl.cu:69); the ring
     // writes every other element of recv, so only the tail needs the copy
     const size_t body = chunk_bytes * (size_t)n;
-    if (send != recv && bytes > body)
-      hip_check(hipMemcpyAsync((char*)recv + body, (const char*)send + body, bytes - body, hipMemcpyDeviceToDevice,
+    if (ksend != krecv && bytes > body)
+      hip_check(hipMemcpyAsync((char*)krecv + body, (const char*)ksend + body, bytes - body, hipMemcpyDefault,
                                stream),
                 "tail copy");
-    CollParams p;
-    memset(&p, 0, sizeof p);
-    p.send = (const char*)send;
-    p.recv = (char*)recv;
-    p.chunk_bytes = chunk_bytes;
-    p.slice_bytes = wave_slice();
-    p.nslices = (chunk_bytes + p.slice_bytes - 1) / p.slice_bytes;
-    const int C = wave_channels();
-    p.iters = (uint32_t)((p.nslices + (uint64_t)C - 1) / (uint64_t)C);
-    p.n = n;
-    p.rank = rank_;
-    p.nslots = cfg_.slots;
-    p.scratch = scratch_;
-    p.mbox = mbox_;
-    p.tx_seq = pair_seq_;
-    p.rx_seq = pair_seq_ + (size_t)n * C;
-    for (int q = 0; q < n; ++q) {
-      p.peer_scratch[q] = peer_scratch_[(size_t)q];
-      p.peer_mbox[q] = peer_mbox_[(size_t)q];
-    }
-    p.status = d_ctl_;
-    p.host_abort = d_ctl_ + 1;
-    p.timeout_ticks = (uint64_t)(cfg_.timeout_ms * 1e5);  // s_memrealtime runs at 100 MHz
-    p.sys_fence = cfg_.sys_fence;
-    // 16-byte vector path whenever every message's local base is dword-aligned (vectors may
-    // straddle 16-byte boundaries on the local side; each message's last len % 16 bytes go
-    // element by element); element-wise path otherwise (2-byte types with odd chunks)
-    const bool vec = (((uintptr_t)send | (uintptr_t)recv) % 4 == 0) && (chunk_bytes % 4 == 0);
-    hipError_t e = algo_ == 1 ? launch_direct(dtype, op, vec, cfg_.channels, cfg_.threads, p, stream)
-                              : launch_ring(dtype, op, vec, cfg_.channels, cfg_.threads, p, stream);
-    hip_check(e, "kernel launch");
+    launch_ring_or_direct(ksend, krecv, chunk_bytes, dtype, op, stream);
+    if (rr == Reach::kStaged) hip_check(hipMemcpyAsync(recv, stage_, bytes, hipMemcpyDefault, stream), "stage out");
   }
   if (cur_dev != device_) hipSetDevice(cur_dev);
   if (cfg_.blocking && cap == hipStreamCaptureStatusNone) return wait_for(stream);

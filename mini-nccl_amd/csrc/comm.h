@@ -47,6 +47,10 @@ class Comm {
   void release();
   void exchange_and_map();
   ncclResult_t wait_for(hipStream_t stream);
+  enum class Reach { kDevice, kMapped, kStaged };
+  Reach reach(const void* p, const void** kernel_ptr) const;
+  void ensure_stage(size_t bytes);
+  void launch_ring_or_direct(const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream);
   ncclResult_t check_status();
 
   int rank_, nranks_, device_ = 0;
@@ -65,6 +69,9 @@ class Comm {
   std::vector<char*> peer_scratch_;
   std::vector<uint64_t*> peer_mbox_;
   std::vector<bool> peer_opened_;  // true: mapped with hipIpcOpenMemHandle (close on destroy)
+
+  char* stage_ = nullptr;         // device staging copy for pageable host buffers (grown on demand)
+  size_t stage_bytes_ = 0;
 
   hipEvent_t done_ = nullptr;
   ncclResult_t sticky_ = ncclSuccess;

@@ -70,8 +70,13 @@ def allreduce_rank(rank, n, port, cases, env, out_q):
             code, npd = O.DTYPES[dtype]
             nbytes = xs[rank].nbytes
             off = case.get("offset", 0)  # misaligned base (bytes) -> scalar path
-            send = hip_rt.DeviceBuffer(nbytes + off)
-            recv = send if inplace else hip_rt.DeviceBuffer(nbytes + off)
+            # where the buffers live: HBM (default), pinned host, or pageable host memory
+            # (a list gives each rank its own placement)
+            def placement(key, dflt):
+                m = case.get(key, dflt)
+                return m[rank % len(m)] if isinstance(m, (list, tuple)) else m
+            send = hip_rt.buffer(placement("mem", "device"), nbytes + off)
+            recv = send if inplace else hip_rt.buffer(placement("recv_mem", placement("mem", "device")), nbytes + off)
             if not inplace:
                 recv.fill_byte(0xAB)
             rc = 0
@@ -85,7 +90,8 @@ def allreduce_rank(rank, n, port, cases, env, out_q):
             dt = time.time() - t0
             got = recv.download(npd, count, off)
             bad, first = compare(got, exp, dtype, op in ("sum", "prod")) if rc == 0 else (-1, -1)
-            results.append({"case": case, "rc": rc, "bad": bad, "first": first, "secs": dt,
+            detail = (f"got {got[first]!r} expected {exp[first]!r}" if bad and first >= 0 else "")
+            results.append({"case": case, "rc": rc, "bad": bad, "first": first, "detail": detail, "secs": dt,
                             "async": comm.async_error()})
             send.free()
             if not inplace:

@@ -25,6 +25,8 @@ def lib():
         _hip.hipFree.argtypes = [vp]
         _hip.hipMemcpy.argtypes = [vp, vp, sz, i]
         _hip.hipMemset.argtypes = [vp, i, sz]
+        _hip.hipHostMalloc.argtypes = [ctypes.POINTER(vp), sz, ctypes.c_uint]
+        _hip.hipHostFree.argtypes = [vp]
         _hip.hipDeviceSynchronize.argtypes = []
         _hip.hipStreamCreate.argtypes = [ctypes.POINTER(vp)]
         _hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_uint]
@@ -42,6 +44,7 @@ def lib():
                   "hipGraphExecDestroy", "hipGraphDestroy"):
             getattr(_hip, f).restype = i
         for f in ("hipSetDevice", "hipGetDeviceCount", "hipMalloc", "hipFree", "hipMemcpy", "hipMemset",
+                  "hipHostMalloc", "hipHostFree",
                   "hipDeviceSynchronize", "hipStreamCreate", "hipStreamCreateWithFlags", "hipStreamSynchronize",
                   "hipStreamDestroy"):
             getattr(_hip, f).restype = i
@@ -80,12 +83,62 @@ class DeviceBuffer:
         return out
 
     def fill_byte(self, value):
+        # hipMemset runs on the null stream and may return before it lands; the test
+        # streams are non-blocking (not ordered after it), so wait here
         check(lib().hipMemset(self.ptr, value, self.nbytes), "hipMemset")
+        check(lib().hipDeviceSynchronize(), "hipDeviceSynchronize")
 
     def free(self):
         if self.ptr:
             lib().hipFree(self.ptr)
             self.ptr = 0
+
+
+class HostBuffer:
+    """Pinned host memory (hipHostMalloc, the reference perf_test's cudaHostAlloc buffers,
+    tests/perf_test.cpp:78-79): the all-reduce kernel addresses it through its device mapping."""
+
+    def __init__(self, nbytes):
+        self.nbytes = nbytes
+        p = ctypes.c_void_p()
+        check(lib().hipHostMalloc(ctypes.byref(p), max(nbytes, 16), 0), "hipHostMalloc")
+        self.ptr = p.value
+
+    def view(self):
+        return np.ctypeslib.as_array((ctypes.c_uint8 * max(self.nbytes, 16)).from_address(self.ptr))
+
+    def upload(self, arr, offset=0):
+        a = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        self.view()[offset:offset + a.size] = a
+
+    def download(self, dtype, count, offset=0):
+        nb = count * np.dtype(dtype).itemsize
+        return self.view()[offset:offset + nb].copy().view(dtype)
+
+    def fill_byte(self, value):
+        self.view()[:] = value
+
+    def free(self):
+        if self.ptr:
+            lib().hipHostFree(self.ptr)
+            self.ptr = 0
+
+
+class PageableBuffer(HostBuffer):
+    """Ordinary (pageable) host memory, unknown to HIP: the library stages it through HBM."""
+
+    def __init__(self, nbytes):
+        self.nbytes = nbytes
+        self._a = np.zeros(max(nbytes, 16) + 64, dtype=np.uint8)
+        self.ptr = (self._a.ctypes.data + 63) & ~63
+
+    def free(self):
+        self._a = None
+        self.ptr = 0
+
+
+def buffer(kind, nbytes):
+    return {"device": DeviceBuffer, "pinned": HostBuffer, "pageable": PageableBuffer}[kind](nbytes)
 
 
 class Stream:

@@ -81,14 +81,15 @@ def _run_allreduce(n, cases, env=None, timeout=300):
         for res in out[r]["results"]:
             c = res["case"]
             assert res["rc"] == 0, f"rank {r} case {c}: ncclResult {res['rc']}"
-            assert res["bad"] == 0, f"rank {r} case {c}: {res['bad']} mismatches, first at {res['first']}"
+            assert res["bad"] == 0, f"rank {r} case {c}: {res['bad']} mismatches, first at {res['first']} {res.get('detail', '')}"
             assert res["async"] == 0
     return out
 
 
-def _case(dtype="f32", op="sum", count=1 << 18, inplace=False, algo=0, calls=1, seed=1234, special=False, offset=0):
+def _case(dtype="f32", op="sum", count=1 << 18, inplace=False, algo=0, calls=1, seed=1234, special=False, offset=0,
+          **kw):
     return dict(dtype=dtype, op=op, count=count, inplace=inplace, algo=algo, calls=calls, seed=seed, special=special,
-                offset=offset)
+                offset=offset, **kw)
 
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
@@ -102,6 +103,26 @@ def test_allreduce_fp32_sum(dev, n, algo):
         _case(count=123457, algo=algo, calls=3, seed=9),     # repeated calls, odd size
     ]
     _run_allreduce(n, cases)
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("stage_host", ["0", "1"], ids=["mapped", "staged"])
+def test_host_buffers(dev, algo, stage_host):
+    # the reference's perf_test hands cudaHostAlloc'd (pinned host) buffers straight to
+    # ncclAllReduce (perf_test.cpp:78-79,88): pinned memory is read and written by the kernel
+    # through its device mapping (or staged with MINI_NCCL_STAGE_HOST=1), pageable memory is
+    # staged through HBM; mixed placements and ranks whose buffers differ must agree
+    cases = [
+        _case(count=(1 << 20) + 3, algo=algo, mem="pinned"),
+        _case(count=(1 << 18) + 1, algo=algo, mem="pinned", inplace=True, seed=5),
+        _case(count=(1 << 19) + 5, algo=algo, mem="pageable", seed=6),
+        _case(count=(1 << 18) + 2, algo=algo, mem="pageable", inplace=True, seed=7),
+        _case(count=200003, algo=algo, mem="device", recv_mem="pinned", seed=8),
+        _case(count=200005, algo=algo, mem="pageable", recv_mem="device", seed=9),
+        _case(dtype="bf16", count=300001, algo=algo, mem="pinned", calls=2, seed=10),
+        _case(count=(1 << 20) + 1, algo=algo, mem=("device", "pinned", "pageable"), seed=11),
+    ]
+    _run_allreduce(3, cases, env={"MINI_NCCL_STAGE_HOST": stage_host})
 
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
