@@ -40,6 +40,8 @@ struct PeerInfo {
   uint64_t host;
   uint64_t slice, scratch_bytes, mbox_bytes;
   int32_t channels, slots, threads, abi;
+  uint64_t min_slice;
+  int32_t depth, pad1;
   hipIpcMemHandle_t scratch_h, mbox_h;
   uint64_t scratch_ptr, mbox_ptr;  // raw addresses for ranks living in the same process
 };
@@ -107,6 +109,8 @@ void Comm::exchange_and_map() {
   me.slots = cfg_.slots;
   me.threads = cfg_.threads;
   me.abi = 1;
+  me.min_slice = cfg_.min_slice;
+  me.depth = cfg_.pipe_depth;
   hip_check(hipIpcGetMemHandle(&me.scratch_h, scratch_), "ipc handle scratch");
   hip_check(hipIpcGetMemHandle(&me.mbox_h, mbox_), "ipc handle mailbox");
   me.scratch_ptr = (uint64_t)(uintptr_t)scratch_;
@@ -119,8 +123,10 @@ void Comm::exchange_and_map() {
     if (p.magic != kInfoMagic || p.rank != q || p.nranks != nranks_)
       throw std::runtime_error("bootstrap: inconsistent rank records");
     if (p.host != me.host) throw std::runtime_error("rank " + std::to_string(q) + " is on another host: only one node is supported");
-    if (p.slice != me.slice || p.channels != me.channels || p.slots != me.slots || p.threads != me.threads)
-      throw std::invalid_argument("MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SLOTS / CHANNELS / THREADS differ between ranks");
+    if (p.slice != me.slice || p.channels != me.channels || p.slots != me.slots || p.threads != me.threads ||
+        p.min_slice != me.min_slice || p.depth != me.depth)
+      throw std::invalid_argument(
+          "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SLOTS / CHANNELS / THREADS / MIN_SLICE / PIPE_DEPTH differ between ranks");
   }
   for (int q = 0; q < nranks_; ++q) {
     if (q == rank_) {
@@ -297,9 +303,10 @@ void Comm::launch_ring_or_direct(const void* send, void* recv, size_t chunk_byte
   p.send = (const char*)send;
   p.recv = (char*)recv;
   p.chunk_bytes = chunk_bytes;
-  p.slice_bytes = wave_slice();
-  p.nslices = (chunk_bytes + p.slice_bytes - 1) / p.slice_bytes;
   const int C = wave_channels();
+  p.slot_bytes = wave_slice();
+  p.slice_bytes = effective_slice(chunk_bytes, C, wave_slice(), cfg_.min_slice, cfg_.pipe_depth);
+  p.nslices = (chunk_bytes + p.slice_bytes - 1) / p.slice_bytes;
   p.iters = (uint32_t)((p.nslices + (uint64_t)C - 1) / (uint64_t)C);
   p.n = n;
   p.rank = rank_;

@@ -55,6 +55,11 @@ Config Config::from_env() {
   }
   c.blocking = env_int("MINI_NCCL_BLOCKING", 1) != 0;
   c.sys_fence = env_int("MINI_NCCL_SYS_FENCE", 1) != 0;
+  long long ms = env_int("MINI_NCCL_MIN_SLICE", 1024);
+  if (ms < 1024) ms = 1024;
+  c.min_slice = (size_t)((ms + 1023) & ~1023LL);
+  c.pipe_depth = (int)env_int("MINI_NCCL_PIPE_DEPTH", 1);
+  if (c.pipe_depth < 1) c.pipe_depth = 1;
   c.stage_host = env_int("MINI_NCCL_STAGE_HOST", 0) != 0;
   c.timeout_ms = (double)env_int("MINI_NCCL_TIMEOUT_MS", 10000);
   if (c.timeout_ms < 1) c.timeout_ms = 1;
@@ -68,10 +73,10 @@ std::string Config::describe() const {
   char b[320];
   snprintf(b, sizeof b,
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, algo=%s, blocking=%d, "
-           "sys_fence=%d, stage_host=%d, timeout=%.0f ms, port=%d",
+           "sys_fence=%d, min_slice=%zu, depth=%d, stage_host=%d, timeout=%.0f ms, port=%d",
            slice_size, window_size, signal_batch, slots, channels, threads,
            algo < 0 ? "auto" : algo ? "direct" : "ring", blocking,
-           sys_fence, stage_host, timeout_ms, port);
+           sys_fence, min_slice, pipe_depth, stage_host, timeout_ms, port);
   return b;
 }
 

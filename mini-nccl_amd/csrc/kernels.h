@@ -14,7 +14,8 @@ struct CollParams {
   const char* send;        // this rank's input (device)
   char* recv;              // this rank's output (device; may equal send)
   uint64_t chunk_bytes;    // (count / n) * elem_size
-  uint64_t slice_bytes;    // bytes per channel message
+  uint64_t slice_bytes;    // payload bytes per channel message (<= slot_bytes)
+  uint64_t slot_bytes;     // scratch slot stride (fixed per communicator: the configured slice)
   uint64_t nslices;        // ceil(chunk_bytes / slice_bytes)
   uint32_t iters;          // ceil(nslices / channels): slices per channel
   int32_t n, rank, nslots;

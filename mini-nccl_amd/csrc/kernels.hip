@@ -341,8 +341,8 @@ __global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
       if (o.recv_msg >= 0) acquire_sys();
       if (len) {
         const u64 coff = (u64)o.chunk * p.chunk_bytes + soff;
-        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, prev, w, rseq), len);
-        const rsrc_t out = make_rsrc(p.peer_scratch[next] + scratch_slot_off(C, K, p.slice_bytes, r, w, sseq), len);
+        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, prev, w, rseq), len);
+        const rsrc_t out = make_rsrc(p.peer_scratch[next] + scratch_slot_off(C, K, p.slot_bytes, r, w, sseq), len);
         const char* lsrc = p.send + coff;
         char* ldst = p.recv + coff;
         switch (o.kind) {
@@ -378,14 +378,14 @@ __device__ __forceinline__ void fold_scalar(const CollParams& p, const char* lsr
     T acc = reinterpret_cast<const T*>(lsrc)[i];
     for (int k = 1; k < n; ++k) {
       const int q = direct_peer(n, r, k);
-      const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q]), nbytes);
+      const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q]), nbytes);
       const T x = __builtin_bit_cast(T, Scal<sizeof(T)>::ld(in, i * (uint32_t)sizeof(T)));
       acc = Op<T, OPC>::f(x, acc);
     }
     reinterpret_cast<T*>(ldst)[i] = acc;
     for (int k = 1; k < n; ++k) {
       const int d = direct_peer(n, r, k);
-      const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slice_bytes, r, w, tx1[d]), nbytes);
+      const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, tx1[d]), nbytes);
       Scal<sizeof(T)>::st(out, i * (uint32_t)sizeof(T), __builtin_bit_cast(Us, acc));
     }
   }
@@ -412,7 +412,7 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
       }
       {
         const int q = direct_peer(n, r, 1);
-        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q]), nbytes);
+        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q]), nbytes);
 #pragma unroll
         for (int u = 0; u < U; ++u)
           if (live[u]) cur[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
@@ -420,7 +420,7 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
       for (int k = 1; k < n; ++k) {
         if (k + 1 < n) {
           const int q = direct_peer(n, r, k + 1);
-          const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q]), nbytes);
+          const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q]), nbytes);
 #pragma unroll
           for (int u = 0; u < U; ++u)
             if (live[u]) nxt[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
@@ -436,7 +436,7 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
         if (live[u]) st_g16(ldst + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
       for (int k = 1; k < n; ++k) {
         const int d = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));  // staggered like phase A
-        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slice_bytes, r, w, tx1[d]), nbytes);
+        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, tx1[d]), nbytes);
 #pragma unroll
         for (int u = 0; u < U; ++u)
           if (live[u]) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
@@ -490,7 +490,7 @@ __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
       const u64 seq0 = tx[d] + itoff;
       if (seq0 + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, d, w), seq0 + 1 - K, ctl, lane)) goto aborted;
       if (len) {
-        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slice_bytes, r, w, seq0), len);
+        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, seq0), len);
         const u64 coff = (u64)d * p.chunk_bytes + soff;
         move<T, OPC, VEC, kSend>(p.send + coff, nullptr, out, out, len, lane);
       }
@@ -541,7 +541,7 @@ __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
     if (len) {
       for (int k = 1; k < n; ++k) {
         const int q = direct_peer(n, r, k);
-        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slice_bytes, q, w, rx0[q] + 1), len);
+        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q] + 1), len);
         const u64 coff = (u64)q * p.chunk_bytes + soff;
         move<T, OPC, VEC, kCopy>(nullptr, p.recv + coff, in, in, len, lane);
       }

@@ -85,6 +85,22 @@ MNCCL_HD uint64_t slice_len(uint64_t chunk_bytes, uint64_t slice_bytes, uint64_t
   return rest < slice_bytes ? rest : slice_bytes;
 }
 
+// Payload bytes per message for one call: the configured slice for large chunks; for chunks
+// too small to give every channel `depth` slices of it, ceil(chunk / (C * depth)) rounded up
+// to whole waves of 16-byte vectors (1 KiB) and at least `min_slice`, so small all-reduces
+// still spread over every pipeline instead of queueing on a few.  A pure function of the
+// call's size and the (rank-uniform) config: every rank picks the same value.  Scratch slot
+// addresses keep the configured stride whatever the payload (scratch_slot_off), so calls of
+// different sizes never alias each other's slots.  Slicing never changes results.
+MNCCL_HD uint64_t effective_slice(uint64_t chunk_bytes, int C, uint64_t slice, uint64_t min_slice, int depth) {
+  if (min_slice >= slice || depth < 1) return slice;
+  const uint64_t per = (uint64_t)C * (uint64_t)depth;
+  uint64_t want = (chunk_bytes + per - 1) / per;
+  want = (want + 1023) & ~(uint64_t)1023;
+  if (want < min_slice) want = min_slice;
+  return want < slice ? want : slice;
+}
+
 // Mailbox layout (uint64 words, one 128-byte line per flag):
 //   READY(src, w)  : written by rank src when its message for this rank landed
 //   CREDIT(dst, w) : written by rank dst when it has consumed a message from this rank

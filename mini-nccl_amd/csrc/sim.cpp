@@ -29,7 +29,7 @@ float apply(int op, float a, float b) {
 
 struct World {
   int n, C, K, op, algo;
-  uint64_t slice, chunk_bytes, nslices;
+  uint64_t slice, slot_bytes, chunk_bytes, nslices;  // payload per message, slot stride
   uint32_t iters;
   std::vector<const float*> send;
   std::vector<float*> recv;
@@ -38,7 +38,7 @@ struct World {
   std::vector<std::vector<uint64_t>> tx_seq, rx_seq;  // per rank: [peer * C + w]
 
   char* slot(int owner, int src, int w, uint64_t seq) {
-    return scratch[owner].data() + scratch_slot_off(C, K, slice, src, w, seq);
+    return scratch[owner].data() + scratch_slot_off(C, K, slot_bytes, src, w, seq);
   }
   uint64_t& ready(int owner, int src, int w) { return mbox[owner][mbox_ready(C, src, w)]; }
   uint64_t& credit(int owner, int dst, int w) { return mbox[owner][mbox_credit(n, C, dst, w)]; }
@@ -173,20 +173,27 @@ bool direct_step(World& W, Prog& P) {
 
 extern "C" {
 
+// csrc/schedule.h effective_slice, exported for the host-logic tests
+uint64_t mnccl_effective_slice(uint64_t chunk_bytes, int channels, uint64_t slice, uint64_t min_slice, int depth) {
+  return effective_slice(chunk_bytes, channels, slice, min_slice, depth);
+}
+
 // Runs `calls` consecutive all-reduces (send -> recv, fp32) on n simulated ranks with the
 // GPU kernels' protocol; call i uses schedule (algo >> i) & 1 (so schedules can alternate
 // on one communicator state, as mncclCommSetAlgo allows).  schedule_seed != 0 permutes the order programs are tried in
 // (pseudo-random), exploring different interleavings.  Returns 0, -1 on deadlock,
 // -2 on bad arguments.  *steps_out = ops executed.
 int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, int n, uint64_t count, int op,
-                        uint64_t slice_bytes, int channels, int slots, int calls, uint64_t schedule_seed,
-                        uint64_t* steps_out) {
+                        uint64_t slice_bytes, uint64_t min_slice, int channels, int slots, int calls,
+                        uint64_t schedule_seed, uint64_t* steps_out) {
   if (n < 1 || n > 16 || channels < 1 || slots < 1 || slice_bytes < 4 || slice_bytes % 4) return -2;
   World W;
-  W.n = n; W.C = channels; W.K = slots; W.op = op; W.algo = algo; W.slice = slice_bytes;
+  W.n = n; W.C = channels; W.K = slots; W.op = op; W.algo = algo; W.slot_bytes = slice_bytes;
   const uint64_t chunk = count / (uint64_t)n;
   W.chunk_bytes = chunk * 4;
-  W.nslices = (W.chunk_bytes + slice_bytes - 1) / slice_bytes;
+  // as Comm::launch_ring_or_direct: adaptive payload (min_slice 0 = off), fixed slot stride
+  W.slice = min_slice ? effective_slice(W.chunk_bytes, channels, slice_bytes, min_slice, 1) : slice_bytes;
+  W.nslices = (W.chunk_bytes + W.slice - 1) / W.slice;
   W.iters = (uint32_t)((W.nslices + (uint64_t)channels - 1) / (uint64_t)channels);
   W.send.assign(send, send + n);
   W.recv.assign(recv, recv + n);

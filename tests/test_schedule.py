@@ -95,3 +95,30 @@ def test_sim_switching_schedules_on_one_communicator(oracle_lib, sim_lib, algos,
     ref = O.allreduce(xs, slice_bytes=64)
     got, _ = S.allreduce(xs, slice_bytes=64, channels=3, slots=2, algos=algos, seed=n)
     assert all(same_bits(g, e) for g, e in zip(got, ref))
+
+
+@pytest.mark.parametrize("chunk", [0, 4, 1000, 1 << 16, (1 << 20) + 12, 3 << 22, 1 << 27, 1 << 30])
+@pytest.mark.parametrize("C", [1, 7, 256])
+def test_effective_slice_properties(sim_lib, chunk, C):
+    # adaptive payload (csrc/schedule.h): never above the configured slice, never below the
+    # floor, whole 1 KiB waves of vectors, and every pipeline busy when it shrinks
+    slice_bytes, floor = 128 * 1024, 1024
+    e = S.effective_slice(chunk, C, slice_bytes, floor)
+    assert floor <= e <= slice_bytes
+    assert e == slice_bytes or e % 1024 == 0
+    nslices = -(-chunk // e)
+    if e < slice_bytes and e > floor:
+        assert nslices <= C and -(-chunk // (e - 1024)) > C  # the smallest payload with <= C slices
+    if chunk >= C * slice_bytes:
+        assert e == slice_bytes
+    assert S.effective_slice(chunk, C, slice_bytes, slice_bytes) == slice_bytes  # MIN_SLICE >= SLICE: off
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("n,count,seed", [(2, 70001, 1), (3, 40000, 2), (4, 9000, 3), (8, 123457, 4)])
+def test_sim_adaptive_slice(oracle_lib, sim_lib, algo, n, count, seed):
+    # payload shrunk below the slot stride, random interleavings over 3 calls: same bits
+    xs = O.random_inputs(n, count, "f32", seed=seed)
+    ref = O.allreduce(xs, slice_bytes=1024)
+    got, _ = S.allreduce(xs, algo=algo, slice_bytes=16384, min_slice=1024, channels=5, slots=2, calls=3, seed=seed)
+    assert all(same_bits(g, e) for g, e in zip(got, ref))
