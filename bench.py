@@ -111,11 +111,11 @@ def cpu_baseline(budget_s=10.0):
 # own communicator (the knobs are read at ncclCommInitRank, as the reference's Config).
 SWEEP_POINTS = [
     # (MINI_NCCL_CHANNELS, MINI_NCCL_THREADS, MINI_NCCL_SLICE_SIZE, algo, MINI_NCCL_SYS_FENCE)
-    (16, 256, 131072, "direct", 1), (32, 256, 131072, "direct", 1), (64, 256, 131072, "direct", 1),
-    (128, 256, 131072, "direct", 1), (64, 256, 524288, "direct", 1), (128, 64, 524288, "direct", 1),
-    (64, 256, 131072, "direct", 0),
-    (16, 256, 131072, "ring", 1), (64, 256, 131072, "ring", 1), (64, 256, 524288, "ring", 1),
-    (128, 64, 524288, "ring", 1), (64, 256, 131072, "ring", 0),
+    (16, 256, 131072, "direct", 0), (32, 256, 131072, "direct", 0), (64, 256, 131072, "direct", 0),
+    (128, 256, 131072, "direct", 0), (64, 256, 524288, "direct", 0), (128, 64, 524288, "direct", 0),
+    (64, 256, 131072, "direct", 1),
+    (16, 256, 131072, "ring", 0), (64, 256, 131072, "ring", 0), (64, 256, 524288, "ring", 0),
+    (128, 64, 524288, "ring", 0), (64, 256, 131072, "ring", 1),
 ]
 C4_SLICES = [65536, 131072, 262144, 1048576]
 C4_WINDOWS = [16, 32, 64]
@@ -147,6 +147,7 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
         torch.cuda.synchronize()
         dt = max_over_ranks(time.perf_counter() - t0)
         ok = comm.async_error() == 0 and bool((recv == float(n)).all().item())
+        ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, torch.float32, M.ncclFloat, st, 1)
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
         return {"GBps": round(count * 4 / (dt / reps) / 1e9, 2), "ok": ok}
     except Exception as e:
@@ -160,6 +161,32 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
             else:
                 os.environ[k] = v
         torch.cuda.empty_cache()
+
+
+def verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream, calls=3):
+    """Cross-rank result check that a protocol race cannot pass: every call gets new,
+    rank- and position-dependent integer-valued inputs (sums exact in any order and in
+    bf16/f16), so a stale or torn slot, a missed hand-off or a wrong chunk owner shows up
+    as a wrong element.  True when every element of every call matches on this rank."""
+    mod = 1021 if tdt == torch.float32 else 8
+    chunk = count // n
+    body = chunk * n
+    ok = True
+    for c in range(calls):
+        idx = torch.arange(count, device=dev, dtype=torch.int64)
+        send.copy_(((idx + 7 * rank + 31 * c) % mod).to(tdt))
+        exp = torch.zeros(count, device=dev, dtype=torch.float32)
+        for q in range(n):
+            exp += ((idx + 7 * q + 31 * c) % mod).to(torch.float32)
+        exp[body:] = send[body:].float()  # the count % n tail keeps this rank's input
+        del idx
+        recv.fill_(-1)
+        torch.cuda.synchronize()
+        rc = comm.all_reduce(send.data_ptr(), recv.data_ptr(), count, ndt, M.ncclSum, stream.cuda_stream)
+        torch.cuda.synchronize()
+        ok = ok and rc == 0 and comm.async_error() == 0 and bool(torch.equal(recv.float(), exp))
+        del exp
+    return ok
 
 
 def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
@@ -339,6 +366,9 @@ def main():
             wall, ev_ms = timed(step, args.steps)
             ae = comm.async_error()
             ok = ok and ae == 0 and bool((recv == float(n)).all().item())
+            # then 3 calls on varying data (outside the timed region), restoring the buffers
+            ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream)
+            send.fill_(1.0)
             ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
             return max_over_ranks(wall), max_over_ranks(ev_ms), ok
 

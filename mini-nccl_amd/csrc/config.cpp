@@ -54,7 +54,7 @@ Config Config::from_env() {
     else throw std::invalid_argument(std::string("MINI_NCCL_ALGO=") + a + " (expected auto|ring|direct)");
   }
   c.blocking = env_int("MINI_NCCL_BLOCKING", 1) != 0;
-  c.sys_fence = env_int("MINI_NCCL_SYS_FENCE", 1) != 0;
+  c.sys_fence = env_int("MINI_NCCL_SYS_FENCE", 0) != 0;
   long long ms = env_int("MINI_NCCL_MIN_SLICE", 1024);
   if (ms < 1024) ms = 1024;
   c.min_slice = (size_t)((ms + 1023) & ~1023LL);

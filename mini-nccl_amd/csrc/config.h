@@ -18,7 +18,7 @@ struct Config {
   int threads = 256;               // MINI_NCCL_THREADS threads per workgroup (one pipeline per wave)
   int algo = -1;                   // MINI_NCCL_ALGO    auto (-1) | ring (0) | direct (1)
   int blocking = 1;                // MINI_NCCL_BLOCKING host waits for the stream (reference behaviour)
-  int sys_fence = 1;               // MINI_NCCL_SYS_FENCE system release fence before each flag
+  int sys_fence = 0;               // MINI_NCCL_SYS_FENCE 1: system release / acquire fences around each hand-off
   size_t min_slice = 1024;         // MINI_NCCL_MIN_SLICE smallest adaptive payload (>= SLICE_SIZE: adaptation off)
   int pipe_depth = 1;              // MINI_NCCL_PIPE_DEPTH slices per pipeline targeted for small calls
   int stage_host = 0;              // MINI_NCCL_STAGE_HOST pinned host buffers: 0 = kernel maps them, 1 = staged copy

@@ -178,7 +178,14 @@ __device__ __noinline__ bool wait_ge(const u64* flag, u64 target, const Ctl& c) 
   }
 }
 
-__device__ __forceinline__ void acquire_sys() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+// After a READY poll.  Every load of handed-off bytes is an sc0 sc1 buffer load of uncached
+// scratch (never L1/L2 resident) and every producer stored them sc0 sc1 and drained before its
+// flag (cdna_hip_programming.md G16 "sc1 loads replace the acquire"), so with
+// MINI_NCCL_SYS_FENCE=0 the fence is only a compiler barrier; =1 keeps the system acquire.
+__device__ __forceinline__ void acquire_sys(int sys_fence) {
+  if (sys_fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // every storing wave: drain its stores (asm so the compiler cannot elide it)
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -338,7 +345,7 @@ __global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
         if (lane == 0) abort_peers(p, C, prev, next);
         return;
       }
-      if (o.recv_msg >= 0) acquire_sys();
+      if (o.recv_msg >= 0) acquire_sys(p.sys_fence);
       if (len) {
         const u64 coff = (u64)o.chunk * p.chunk_bytes + soff;
         const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, prev, w, rseq), len);
@@ -513,7 +520,7 @@ __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
       if (tx1[q] + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, q, w), tx1[q] + 1 - K, ctl, lane))
         goto aborted;
     }
-    acquire_sys();
+    acquire_sys(p.sys_fence);
     if (len) {
       const u64 coff = (u64)r * p.chunk_bytes + soff;
       fold_and_push<T, OPC, VEC>(p, p.send + coff, p.recv + coff, rx0, tx1, len, w, C, lane);
@@ -537,7 +544,7 @@ __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
       const int q = direct_peer(n, r, k);
       if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 2, ctl, lane)) goto aborted;
     }
-    acquire_sys();
+    acquire_sys(p.sys_fence);
     if (len) {
       for (int k = 1; k < n; ++k) {
         const int q = direct_peer(n, r, k);

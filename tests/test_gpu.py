@@ -126,6 +126,14 @@ def test_host_buffers(dev, algo, stage_host):
 
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+def test_sys_fence_on(dev, algo):
+    # MINI_NCCL_SYS_FENCE=1: system release / acquire fences around every hand-off (the
+    # default relies on sc0 sc1 payload accesses of uncached scratch instead)
+    cases = [_case(count=(1 << 20) + 1, algo=algo, seed=21), _case(dtype="bf16", count=77777, algo=algo, seed=22)]
+    _run_allreduce(3, cases, env={"MINI_NCCL_SYS_FENCE": "1"})
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
 def test_allreduce_8_ranks(dev, algo):
     # the 8-GPU node's rank count, all on GPU 0: every pair of the mesh is exercised
     cases = [_case(count=(1 << 20) + 5, algo=algo, seed=8), _case(dtype="bf16", count=(1 << 19) + 3, algo=algo,
