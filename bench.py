@@ -111,11 +111,10 @@ def cpu_baseline(budget_s=10.0):
 # own communicator (the knobs are read at ncclCommInitRank, as the reference's Config).
 SWEEP_POINTS = [
     # (MINI_NCCL_CHANNELS, MINI_NCCL_THREADS, MINI_NCCL_SLICE_SIZE, algo, MINI_NCCL_SYS_FENCE)
-    (16, 256, 131072, "direct", 0), (32, 256, 131072, "direct", 0), (64, 256, 131072, "direct", 0),
-    (128, 256, 131072, "direct", 0), (64, 256, 524288, "direct", 0), (128, 64, 524288, "direct", 0),
-    (64, 256, 131072, "direct", 1),
-    (16, 256, 131072, "ring", 0), (64, 256, 131072, "ring", 0), (64, 256, 524288, "ring", 0),
-    (128, 64, 524288, "ring", 0), (64, 256, 131072, "ring", 1),
+    (256, 64, 131072, "direct", 0), (64, 256, 131072, "direct", 0), (256, 128, 131072, "direct", 0),
+    (128, 64, 131072, "direct", 0), (256, 64, 524288, "direct", 0), (256, 64, 131072, "direct", 1),
+    (256, 64, 131072, "ring", 0), (64, 256, 131072, "ring", 0), (256, 128, 131072, "ring", 0),
+    (128, 64, 131072, "ring", 0), (256, 64, 524288, "ring", 0), (256, 64, 131072, "ring", 1),
 ]
 C4_SLICES = [65536, 131072, 262144, 1048576]
 C4_WINDOWS = [16, 32, 64]

@@ -39,10 +39,14 @@ Config Config::from_env() {
   if (c.slots < 2) c.slots = 2;
   if (c.slots > 64) c.slots = 64;
   c.channels = (int)env_int("MINI_NCCL_CHANNELS", 0);
-  if (c.channels <= 0) c.channels = c.window_size;  // workgroups; each wave is one pipeline
+  // workgroups; each wave is one pipeline.  Default 4 x WINDOW one-wave workgroups (256 at the
+  // reference's WINDOW 64): one pipeline per CU of the 256, so no two pipelines share a CU's
+  // L1 / address path (2 ranks on one GPU: 372 -> 791 GB/s against 64 four-wave workgroups,
+  // profiles/r1_geometry_sweep.txt)
+  if (c.channels <= 0) c.channels = 4 * c.window_size;
   if (c.channels < 1) c.channels = 1;
-  if (c.channels > 256) c.channels = 256;
-  c.threads = (int)env_int("MINI_NCCL_THREADS", 256);
+  if (c.channels > 1024) c.channels = 1024;
+  c.threads = (int)env_int("MINI_NCCL_THREADS", 64);
   if (c.threads < 64) c.threads = 64;
   if (c.threads > 1024) c.threads = 1024;
   c.threads &= ~63;
@@ -60,6 +64,7 @@ Config Config::from_env() {
   c.min_slice = (size_t)((ms + 1023) & ~1023LL);
   c.pipe_depth = (int)env_int("MINI_NCCL_PIPE_DEPTH", 1);
   if (c.pipe_depth < 1) c.pipe_depth = 1;
+  c.direct_overlap = env_int("MINI_NCCL_DIRECT_OVERLAP", 1) != 0;
   c.stage_host = env_int("MINI_NCCL_STAGE_HOST", 0) != 0;
   c.timeout_ms = (double)env_int("MINI_NCCL_TIMEOUT_MS", 10000);
   if (c.timeout_ms < 1) c.timeout_ms = 1;

@@ -14,13 +14,14 @@ struct Config {
   int signal_batch = 16;           // MINI_NCCL_SIGNAL_BATCH (validated)
   // this build's knobs
   int slots = 2;                   // MINI_NCCL_SLOTS   scratch slots per channel (>= 2; 2 = double buffer)
-  int channels = 0;                // MINI_NCCL_CHANNELS (0 -> window_size)
-  int threads = 256;               // MINI_NCCL_THREADS threads per workgroup (one pipeline per wave)
+  int channels = 0;                // MINI_NCCL_CHANNELS workgroups (0 -> 4 x window_size)
+  int threads = 64;                // MINI_NCCL_THREADS threads per workgroup (one pipeline per wave)
   int algo = -1;                   // MINI_NCCL_ALGO    auto (-1) | ring (0) | direct (1)
   int blocking = 1;                // MINI_NCCL_BLOCKING host waits for the stream (reference behaviour)
   int sys_fence = 0;               // MINI_NCCL_SYS_FENCE 1: system release / acquire fences around each hand-off
   size_t min_slice = 1024;         // MINI_NCCL_MIN_SLICE smallest adaptive payload (>= SLICE_SIZE: adaptation off)
   int pipe_depth = 1;              // MINI_NCCL_PIPE_DEPTH slices per pipeline targeted for small calls
+  int direct_overlap = 1;          // MINI_NCCL_DIRECT_OVERLAP next iteration's raw pushes before this one's results
   int stage_host = 0;              // MINI_NCCL_STAGE_HOST pinned host buffers: 0 = kernel maps them, 1 = staged copy
   double timeout_ms = 10000.0;     // MINI_NCCL_TIMEOUT_MS (reference watchdog: 10 s)
   int port = 8888;                 // MINI_NCCL_PORT   bootstrap port (reference: 8888)

@@ -29,6 +29,7 @@ struct CollParams {
   const uint32_t* host_abort;  // host-mapped abort request
   uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
   int32_t sys_fence;       // system-scope release fence before each ready flag
+  int32_t direct_overlap;  // direct: next iteration's raw pushes before this one's results
 };
 
 constexpr int kMaxRanks = 16;

@@ -398,6 +398,11 @@ __device__ __forceinline__ void fold_scalar(const CollParams& p, const char* lsr
   }
 }
 
+#ifndef MNCCL_FOLD_U
+#define MNCCL_FOLD_U 8
+#endif
+constexpr int kFoldU = MNCCL_FOLD_U;  // vectors per lane per batch in the fold (as kU for moves)
+
 // Fold of the n-1 arriving slices of this rank's own chunk, software-pipelined by one
 // peer so two slot loads per vector are in flight; acc = op(x_q, acc) in ring order.
 // rx0[q]: sequence number of q's raw message for this slice; tx1[d]: of my result message to d
@@ -406,7 +411,7 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
                                               const u64* tx1, uint32_t nbytes, int w, int C, int lane) {
   const int n = p.n, r = p.rank, K = p.nslots;
   if (VEC) {
-    constexpr int U = 4;
+    constexpr int U = kFoldU;
     const uint32_t nvec = nbytes >> 4;
     for (uint32_t b = 0; b < nvec; b += 64 * U) {
       v4u acc[U], cur[U], nxt[U];
@@ -477,7 +482,11 @@ __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
   }
   __builtin_amdgcn_wave_barrier();
 
-  for (uint32_t it = 0; it < p.iters; ++it) {
+  const uint32_t nsteps = 3 * p.iters;
+  for (uint32_t j = 0; j < nsteps; ++j) {
+    int phase;
+    uint32_t it;
+    direct_phase_at(j, p.iters, p.direct_overlap, &phase, &it);
     const u64 s = (u64)it * C + w;
     const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
     const u64 soff = s * p.slice_bytes;
@@ -488,76 +497,79 @@ __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
     }
     __builtin_amdgcn_wave_barrier();
 
-    // Phase A: push my raw slice of chunk d to rank d, for every peer d; one drain for all
-    // n-1 pushes, then the n-1 READY flags.  Pipeline w starts at peer (w mod n-1): the
-    // pipelines of a rank spread over all n-1 xGMI links instead of marching through them
-    // one link at a time (the push order does not touch the fold order).
-    for (int k = 1; k < n; ++k) {
-      const int d = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));
-      const u64 seq0 = tx[d] + itoff;
-      if (seq0 + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, d, w), seq0 + 1 - K, ctl, lane)) goto aborted;
+    if (phase == 0) {
+      // Phase A: push my raw slice of chunk d to rank d, for every peer d; one drain for all
+      // n-1 pushes, then the n-1 READY flags.  Pipeline w starts at peer (w mod n-1): the
+      // pipelines of a rank spread over all n-1 xGMI links instead of marching through them
+      // one link at a time (the push order does not touch the fold order).
+      for (int k = 1; k < n; ++k) {
+        const int d = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));
+        const u64 seq0 = tx[d] + itoff;
+        if (seq0 + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, d, w), seq0 + 1 - K, ctl, lane))
+          goto aborted;
+        if (len) {
+          const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, seq0), len);
+          const u64 coff = (u64)d * p.chunk_bytes + soff;
+          move<T, OPC, VEC, kSend>(p.send + coff, nullptr, out, out, len, lane);
+        }
+      }
+      drain_stores();
+      if (lane == 0) {
+        if (p.sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int k = 1; k < n; ++k) {
+          const int d = direct_peer(n, r, k);
+          st_sys(p.peer_mbox[d] + mbox_ready(C, r, w), tx[d] + itoff + 1);
+        }
+      }
+    } else if (phase == 1) {
+      // Phase B: wait for the n-1 raw slices of my chunk and for slot credits of the
+      // result message at every peer; fold; store; push the result everywhere.
+      for (int k = 1; k < n; ++k) {
+        const int q = direct_peer(n, r, k);
+        if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 1, ctl, lane)) goto aborted;
+        if (tx1[q] + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, q, w), tx1[q] + 1 - K, ctl, lane))
+          goto aborted;
+      }
+      acquire_sys(p.sys_fence);
       if (len) {
-        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, seq0), len);
-        const u64 coff = (u64)d * p.chunk_bytes + soff;
-        move<T, OPC, VEC, kSend>(p.send + coff, nullptr, out, out, len, lane);
+        const u64 coff = (u64)r * p.chunk_bytes + soff;
+        fold_and_push<T, OPC, VEC>(p, p.send + coff, p.recv + coff, rx0, tx1, len, w, C, lane);
       }
-    }
-    drain_stores();
-    if (lane == 0) {
-      if (p.sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      for (int k = 1; k < n; ++k) {
-        const int d = direct_peer(n, r, k);
-        st_sys(p.peer_mbox[d] + mbox_ready(C, r, w), tx[d] + itoff + 1);
+      drain_stores();
+      if (lane == 0) {
+        for (int k = 1; k < n; ++k) {
+          const int q = direct_peer(n, r, k);
+          st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), rx0[q] + 1);  // raw slot consumed
+        }
+        if (p.sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int k = 1; k < n; ++k) {
+          const int d = direct_peer(n, r, k);
+          st_sys(p.peer_mbox[d] + mbox_ready(C, r, w), tx1[d] + 1);
+        }
       }
-    }
-
-    // Phase B: wait for the n-1 raw slices of my chunk and for slot credits of the
-    // result message at every peer; fold; store; push the result everywhere.
-    for (int k = 1; k < n; ++k) {
-      const int q = direct_peer(n, r, k);
-      if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 1, ctl, lane)) goto aborted;
-      if (tx1[q] + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, q, w), tx1[q] + 1 - K, ctl, lane))
-        goto aborted;
-    }
-    acquire_sys(p.sys_fence);
-    if (len) {
-      const u64 coff = (u64)r * p.chunk_bytes + soff;
-      fold_and_push<T, OPC, VEC>(p, p.send + coff, p.recv + coff, rx0, tx1, len, w, C, lane);
-    }
-    drain_stores();
-    if (lane == 0) {
+    } else {
+      // Phase C: wait for every peer's result slice, store them all, one drain, n-1 credits
       for (int k = 1; k < n; ++k) {
         const int q = direct_peer(n, r, k);
-        st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), rx0[q] + 1);  // raw slot consumed
+        if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 2, ctl, lane)) goto aborted;
       }
-      if (p.sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      for (int k = 1; k < n; ++k) {
-        const int d = direct_peer(n, r, k);
-        st_sys(p.peer_mbox[d] + mbox_ready(C, r, w), tx1[d] + 1);
+      acquire_sys(p.sys_fence);
+      if (len) {
+        for (int k = 1; k < n; ++k) {
+          const int q = direct_peer(n, r, k);
+          const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q] + 1), len);
+          const u64 coff = (u64)q * p.chunk_bytes + soff;
+          move<T, OPC, VEC, kCopy>(nullptr, p.recv + coff, in, in, len, lane);
+        }
       }
-    }
-
-    // Phase C: wait for every peer's result slice, store them all, one drain, n-1 credits
-    for (int k = 1; k < n; ++k) {
-      const int q = direct_peer(n, r, k);
-      if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 2, ctl, lane)) goto aborted;
-    }
-    acquire_sys(p.sys_fence);
-    if (len) {
-      for (int k = 1; k < n; ++k) {
-        const int q = direct_peer(n, r, k);
-        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q] + 1), len);
-        const u64 coff = (u64)q * p.chunk_bytes + soff;
-        move<T, OPC, VEC, kCopy>(nullptr, p.recv + coff, in, in, len, lane);
-      }
-    }
-    drain_stores();
-    if (lane == 0) {
-      for (int k = 1; k < n; ++k) {
-        const int q = direct_peer(n, r, k);
-        st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), rx0[q] + 2);
+      drain_stores();
+      if (lane == 0) {
+        for (int k = 1; k < n; ++k) {
+          const int q = direct_peer(n, r, k);
+          st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), rx0[q] + 2);
+        }
       }
     }
   }

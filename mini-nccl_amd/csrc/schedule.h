@@ -75,6 +75,30 @@ MNCCL_HD RingOp ring_op(int n, int r, int k) {
 MNCCL_HD int direct_peer(int n, int r, int k) { return mod_n(r + k, n); }  // k = 1..n-1
 MNCCL_HD int direct_msgs_per_iter() { return 2; }  // per (pair, channel): raw, then final
 
+// Direct phases of one pipeline, in execution order: A(t) pushes raw slices of iteration t,
+// B(t) folds and pushes results, C(t) copies the arriving results.  Plain order A0 B0 C0 A1 B1
+// C1 ...; overlapped order A0 B0 A1 C0 B1 A2 C1 ... B(I-1) C(I-1): the next iteration's raw
+// pushes go out before this iteration's results are awaited, so a pipeline always has a
+// message in flight.  Deadlock-free with 2 slots: A(t+1) needs each peer's B(t) (the credit
+// for raw(t)), which needs only this rank's A(t) and C(t-1), both earlier in the order
+// (tests/test_schedule.py runs both orders under random interleavings).
+MNCCL_HD void direct_phase_at(uint32_t j, uint32_t iters, int overlap, int* phase, uint32_t* it) {
+  if (!overlap) {
+    *phase = (int)(j % 3);
+    *it = j / 3;
+    return;
+  }
+  if (j == 0) {
+    *phase = 0;
+    *it = 0;
+    return;
+  }
+  const uint32_t t = (j - 1) / 3, m = (j - 1) % 3;
+  if (m == 0) { *phase = 1; *it = t; }
+  else if (m == 1 && t + 1 < iters) { *phase = 0; *it = t + 1; }
+  else { *phase = 2; *it = t; }
+}
+
 // Slice geometry shared by both schedules: channel w owns slices w, w+C, w+2C, ...
 // of every chunk; message bytes of slice s (0 for the padding slices past the end, which
 // still move flags so every channel sends the same number of messages).

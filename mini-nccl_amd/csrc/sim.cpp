@@ -28,7 +28,7 @@ float apply(int op, float a, float b) {
 }
 
 struct World {
-  int n, C, K, op, algo;
+  int n, C, K, op, algo, overlap = 1;
   uint64_t slice, slot_bytes, chunk_bytes, nslices;  // payload per message, slot stride
   uint32_t iters;
   std::vector<const float*> send;
@@ -63,7 +63,8 @@ void do_move(int kind, int op, const float* local, const float* in, float* recv,
 struct Prog {
   int r, w;
   uint32_t it = 0;
-  int k = 0;  // op index within the iteration
+  int k = 0;      // ring: op index within the iteration
+  uint32_t j = 0; // direct: phase step (direct_phase_at)
   bool done = false;
 };
 
@@ -103,14 +104,17 @@ bool ring_step(World& W, Prog& P) {
 // credits).  A phase publishes nothing until its end, as the kernel's single drain per phase.
 bool direct_step(World& W, Prog& P) {
   const int n = W.n, r = P.r, w = P.w, K = W.K;
-  const uint64_t s = (uint64_t)P.it * W.C + w;
+  int phase;
+  uint32_t it;
+  direct_phase_at(P.j, W.iters, W.overlap, &phase, &it);
+  const uint64_t s = (uint64_t)it * W.C + w;
   const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
   const uint64_t soff = s * W.slice;
-  const uint64_t itoff = (uint64_t)P.it * direct_msgs_per_iter();
+  const uint64_t itoff = (uint64_t)it * direct_msgs_per_iter();
   // per-pair FIFO positions: raw message of this iteration = +0, result = +1
   auto tx0 = [&](int d) { return W.tx_seq[r][(size_t)d * W.C + w] + itoff; };
   auto rx0 = [&](int q) { return W.rx_seq[r][(size_t)q * W.C + w] + itoff; };
-  if (P.k == 0) {
+  if (phase == 0) {
     for (int k = 1; k < n; ++k) {
       const int d = direct_peer(n, r, k);
       if (tx0(d) + 1 > (uint64_t)K && W.credit(r, d, w) < tx0(d) + 1 - K) return false;
@@ -124,7 +128,7 @@ bool direct_step(World& W, Prog& P) {
       }
     }
     for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx0(direct_peer(n, r, k)) + 1;
-  } else if (P.k == 1) {
+  } else if (phase == 1) {
     for (int k = 1; k < n; ++k) {
       const int q = direct_peer(n, r, k);
       if (W.ready(r, q, w) < rx0(q) + 1) return false;
@@ -162,10 +166,7 @@ bool direct_step(World& W, Prog& P) {
     }
     for (int k = 1; k < n; ++k) W.credit(direct_peer(n, r, k), r, w) = rx0(direct_peer(n, r, k)) + 2;
   }
-  if (++P.k == 3) {
-    P.k = 0;
-    if (++P.it == W.iters) P.done = true;
-  }
+  if (++P.j == 3 * W.iters) P.done = true;
   return true;
 }
 
@@ -174,6 +175,9 @@ bool direct_step(World& W, Prog& P) {
 extern "C" {
 
 // csrc/schedule.h effective_slice, exported for the host-logic tests
+void mnccl_direct_phase_at(uint32_t j, uint32_t iters, int overlap, int* phase, uint32_t* it) {
+  direct_phase_at(j, iters, overlap, phase, it);
+}
 uint64_t mnccl_effective_slice(uint64_t chunk_bytes, int channels, uint64_t slice, uint64_t min_slice, int depth) {
   return effective_slice(chunk_bytes, channels, slice, min_slice, depth);
 }
@@ -184,11 +188,12 @@ uint64_t mnccl_effective_slice(uint64_t chunk_bytes, int channels, uint64_t slic
 // (pseudo-random), exploring different interleavings.  Returns 0, -1 on deadlock,
 // -2 on bad arguments.  *steps_out = ops executed.
 int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, int n, uint64_t count, int op,
-                        uint64_t slice_bytes, uint64_t min_slice, int channels, int slots, int calls,
-                        uint64_t schedule_seed, uint64_t* steps_out) {
+                        uint64_t slice_bytes, uint64_t min_slice, int direct_overlap, int channels, int slots,
+                        int calls, uint64_t schedule_seed, uint64_t* steps_out) {
   if (n < 1 || n > 16 || channels < 1 || slots < 1 || slice_bytes < 4 || slice_bytes % 4) return -2;
   World W;
   W.n = n; W.C = channels; W.K = slots; W.op = op; W.algo = algo; W.slot_bytes = slice_bytes;
+  W.overlap = direct_overlap;
   const uint64_t chunk = count / (uint64_t)n;
   W.chunk_bytes = chunk * 4;
   // as Comm::launch_ring_or_direct: adaptive payload (min_slice 0 = off), fixed slot stride

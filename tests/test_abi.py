@@ -136,14 +136,14 @@ def test_config_from_env(sim_lib, monkeypatch):
             monkeypatch.delenv(k)
     rc, s = S.config_describe()
     assert rc == 0
-    # reference defaults (Config.h:29-47): 128 KiB, 64, 16; workgroups = window
-    assert "SLICE_SIZE=131072 B" in s and "WINDOW=64" in s and "BATCH=16" in s and "channels=64" in s
-    assert "algo=auto" in s and "threads=256" in s
+    # reference defaults (Config.h:29-47): 128 KiB, 64, 16; one-wave workgroups = 4 x window
+    assert "SLICE_SIZE=131072 B" in s and "WINDOW=64" in s and "BATCH=16" in s and "channels=256" in s
+    assert "algo=auto" in s and "threads=64" in s and "sys_fence=0" in s and "min_slice=1024" in s
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", "0")       # Config.h:50: 0 -> 1024
     monkeypatch.setenv("MINI_NCCL_WINDOW_SIZE", "-3")     # Config.h:51: <= 0 -> 1
     monkeypatch.setenv("MINI_NCCL_SLOTS", "1")            # clamped to 2 (deadlock-free minimum)
     rc, s = S.config_describe()
-    assert "SLICE_SIZE=1024 B" in s and "WINDOW=1" in s and "slots=2" in s and "channels=1" in s
+    assert "SLICE_SIZE=1024 B" in s and "WINDOW=1" in s and "slots=2" in s and "channels=4" in s
     monkeypatch.setenv("MINI_NCCL_ALGO", "direct")
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", "100")     # rounded down to whole 16-byte vectors
     rc, s = S.config_describe()

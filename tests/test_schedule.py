@@ -122,3 +122,29 @@ def test_sim_adaptive_slice(oracle_lib, sim_lib, algo, n, count, seed):
     ref = O.allreduce(xs, slice_bytes=1024)
     got, _ = S.allreduce(xs, algo=algo, slice_bytes=16384, min_slice=1024, channels=5, slots=2, calls=3, seed=seed)
     assert all(same_bits(g, e) for g, e in zip(got, ref))
+
+
+@pytest.mark.parametrize("overlap", [0, 1], ids=["plain", "overlapped"])
+@pytest.mark.parametrize("seed", range(1, 9))
+def test_sim_direct_phase_orders(oracle_lib, sim_lib, overlap, seed):
+    # both direct phase orders (csrc/schedule.h direct_phase_at) under random interleavings,
+    # several iterations per pipeline, 2 and 3 slots: same bits, no deadlock
+    n = 2 + seed % 7
+    xs = O.random_inputs(n, 5000 + 13 * seed, "f32", seed=seed)
+    ref = O.allreduce(xs, slice_bytes=64)
+    got, _ = S.allreduce(xs, algo=1, slice_bytes=64, channels=1 + seed % 3, slots=2 + seed % 2, calls=2,
+                         seed=seed, direct_overlap=overlap)
+    assert all(same_bits(g, e) for g, e in zip(got, ref))
+
+
+def test_direct_phase_order_is_a_permutation(sim_lib):
+    # every (phase, iteration) exactly once, A(t) before B(t) before C(t), A(t+1) before C(t)
+    for iters in (1, 2, 3, 7):
+        for overlap in (0, 1):
+            seen = [S.direct_phase_at(j, iters, overlap) for j in range(3 * iters)]
+            assert sorted(seen) == sorted((ph, t) for t in range(iters) for ph in range(3))
+            pos = {x: i for i, x in enumerate(seen)}
+            for t in range(iters):
+                assert pos[(0, t)] < pos[(1, t)] < pos[(2, t)]
+                if overlap and t + 1 < iters:
+                    assert pos[(0, t + 1)] < pos[(2, t)]
