@@ -413,45 +413,53 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
   if (VEC) {
     constexpr int U = kFoldU;
     const uint32_t nvec = nbytes >> 4;
-    for (uint32_t b = 0; b < nvec; b += 64 * U) {
+    uint32_t b = 0;
+    // full batches, no per-vector predicate: every lane has U loads per stream in flight
+    // (a predicated batch made the compiler wait on each load before issuing the next)
+    for (; b + 64 * U <= nvec; b += 64 * U) {
       v4u acc[U], cur[U], nxt[U];
-      bool live[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t i = b + (uint32_t)(u * 64 + lane);
-        live[u] = i < nvec;
-        if (live[u]) acc[u] = ld_g16(lsrc + (size_t)i * 16);
-      }
+      for (int u = 0; u < U; ++u) acc[u] = ld_g16(lsrc + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16);
       {
         const int q = direct_peer(n, r, 1);
         const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q]), nbytes);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (live[u]) cur[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
+        for (int u = 0; u < U; ++u) cur[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
       }
       for (int k = 1; k < n; ++k) {
         if (k + 1 < n) {
           const int q = direct_peer(n, r, k + 1);
           const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q]), nbytes);
 #pragma unroll
-          for (int u = 0; u < U; ++u)
-            if (live[u]) nxt[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
+          for (int u = 0; u < U; ++u) nxt[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (live[u]) acc[u] = reduce16<T, OPC>(cur[u], acc[u]);
+        for (int u = 0; u < U; ++u) acc[u] = reduce16<T, OPC>(cur[u], acc[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) cur[u] = nxt[u];
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (live[u]) st_g16(ldst + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
+      for (int u = 0; u < U; ++u) st_g16(ldst + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
       for (int k = 1; k < n; ++k) {
         const int d = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));  // staggered like phase A
         const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, tx1[d]), nbytes);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (live[u]) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
+        for (int u = 0; u < U; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
+      }
+    }
+    // the rest: one vector per lane
+    for (uint32_t i = b + (uint32_t)lane; i < nvec; i += 64) {
+      v4u acc = ld_g16(lsrc + (size_t)i * 16);
+      for (int k = 1; k < n; ++k) {
+        const int q = direct_peer(n, r, k);
+        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q]), nbytes);
+        acc = reduce16<T, OPC>(ld_slot16(in, i * 16), acc);
+      }
+      st_g16(ldst + (size_t)i * 16, acc);
+      for (int k = 1; k < n; ++k) {
+        const int d = direct_peer(n, r, k);
+        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, tx1[d]), nbytes);
+        st_slot16(out, i * 16, acc);
       }
     }
     if (nbytes & 15u) fold_scalar<T, OPC>(p, lsrc, ldst, rx0, tx1, nbytes, w, C, lane, nvec * 16);
