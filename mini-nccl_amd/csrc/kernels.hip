@@ -1,30 +1,33 @@
 // kernels.hip -- the hot path, hand-written for CDNA4 (gfx950).
 //
 //  ring_kernel    persistent ring all-reduce (reference mini_nccl.cu:56-217 re-designed):
-//                 one workgroup per channel, each an independent slice pipeline; the
+//                 one WAVE per pipeline (channel), each an independent slice pipeline; the
 //                 reference's per-slice launches of wait_kernel (:22-30),
 //                 elementwise_reduce_kernel (:43-47), the IPC memcpy (:131,:174) and
 //                 set_flag_kernel (:32-36) become one launch per call in which every
-//                 channel moves its slices through a `slots`-deep FIFO in the next
+//                 pipeline moves its slices through a `slots`-deep FIFO in the next
 //                 rank's scratch with epoch-free monotone flags and explicit credits.
+//                 Default geometry: 256 one-wave workgroups = one pipeline per CU.
 //  direct_kernel  same association order, every peer link at once (schedule.h).
 //  local_reduce   the element-wise op alone: out = op(local, incoming), 16 B per lane.
 //
 // Memory-ordering protocol (cross-process, cross-device over xGMI):
 //  * everything another rank writes lives in THIS rank's scratch / mailbox, allocated
 //    hipDeviceMallocUncached: no cache of any agent keeps a copy of those lines;
-//  * payload stores to a peer's slot are system-coherent (sc0 sc1) 16-byte buffer
-//    stores; every storing wave drains (s_waitcnt vmcnt(0)), the workgroup barriers,
-//    lane 0 optionally issues a system-scope release fence, drains again (asm, so the
-//    compiler cannot drop it) and stores the READY word with a system-scope atomic;
-//  * the consumer polls its own READY word with system-scope relaxed loads from one
-//    lane (s_sleep between polls), then one system-scope acquire fence, a barrier, and
-//    reads the slot with sc0 sc1 loads (which bypass L1/L2 regardless of mapping);
-//  * after the barrier that follows the last load of a slot, lane 0 returns a CREDIT to
+//  * payload stores to a peer's slot are sc0 sc1 16-byte buffer stores (the instruction a
+//    system-scope atomic store is; write-through, nothing left dirty in an L2); the wave
+//    drains (s_waitcnt vmcnt(0) in asm, so the compiler cannot drop it) and lane 0 stores
+//    the READY word with a system-scope atomic store;
+//  * the consumer polls its own READY word with system-scope relaxed loads from lane 0
+//    (s_sleep between polls) and reads the slot with sc0 sc1 loads (system-scope atomic
+//    loads: they bypass L1/L2 whatever the mapping), so neither a release fence before
+//    the flag nor an acquire fence after the poll is needed (cdna_hip_programming.md
+//    Guideline 16's sc1 form); MINI_NCCL_SYS_FENCE=1 adds both (system scope);
+//  * after the drain that follows the last load of a slot, lane 0 returns a CREDIT to
 //    the sender; the sender reuses a slot only after the credit for the message that
 //    last used it (seq - slots) arrived.
-//  * flags are monotone 64-bit sequence numbers that continue across calls (per-channel
-//    base kept in device memory and advanced by the kernel itself, so graph replays stay
+//  * flags are monotone 64-bit sequence numbers per (peer, pipeline) that continue across
+//    calls (kept in device memory and advanced by the kernel itself, so graph replays stay
 //    consistent); nothing is reset per call and stale flags cannot satisfy a wait.
 //  * every spin is bounded (MINI_NCCL_TIMEOUT_MS via s_memrealtime) and also exits on
 //    the host abort word or a peer's ABORT; the kernel always terminates.
@@ -190,7 +193,7 @@ __device__ __forceinline__ void acquire_sys(int sys_fence) {
 // every storing wave: drain its stores (asm so the compiler cannot elide it)
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// lane 0, after the workgroup barrier that follows every wave's drain
+// lane 0, after its wave's drain
 __device__ __forceinline__ void publish(u64* flag, u64 v, int sys_fence) {
   if (sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -199,8 +202,8 @@ __device__ __forceinline__ void publish(u64* flag, u64 v, int sys_fence) {
 
 // ---------------------------------------------------------------- wave-level sync
 // A channel is ONE wave (64 lanes): lane 0 polls and signals, the wave's own s_waitcnt orders
-// its memory operations, and no workgroup barrier is ever needed -- the 16 waves of a
-// workgroup are 16 independent pipelines that hide each other's hand-off latency.
+// its memory operations, and no workgroup barrier is ever needed -- the waves of a
+// workgroup (one by default) are independent pipelines.
 __device__ __forceinline__ bool wave_wait_ge(const u64* flag, u64 target, const Ctl& c, int lane) {
   int ok = 1;
   if (lane == 0) ok = wait_ge(flag, target, c) ? 1 : 0;
