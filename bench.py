@@ -422,6 +422,14 @@ def main():
                           "kernel": kern_key, "kernel_ms": round(ev_ms, 4), "alg_bytes_per_launch": alg_bytes}
     if traffic is not None:
         result["roofline"]["traffic_source"] = tsrc
+    if n > 1:
+        # `achieved` counts SURVEY.md §8(d)'s sum-kernel bytes only; the fused kernel also does
+        # the raw send and the all-gather: every byte one rank reads or writes, local or pushed
+        # to a peer, is esz * chunk * (6n - 4) for both schedules (Kernels)
+        fused = esz * (count // n) * (6 * n - 4)
+        fa = fused / (ev_ms / 1e3) / 1e9
+        result["roofline"].update({"fused_alg_bytes_per_launch": fused, "fused_achieved": round(fa, 2),
+                                   "fused_frac": round(fa / HBM_PEAK_GBS, 4)})
     if n > 1 and not args.no_alt:
         # the comparison ceiling: RCCL's all-reduce on the same buffer (torch.distributed nccl)
         try:
