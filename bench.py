@@ -106,15 +106,18 @@ def cpu_baseline(budget_s=10.0):
 
 
 # ------------------------------------------------------------------ N > 1 configuration sweeps
-# (workgroups, threads, slice, algo, sys_fence) points timed on a 256 MiB buffer, and the
+# (schedule, knob) points timed on a 256 MiB buffer, and the
 # BASELINE.json configs[3] (C4) grid: ring, 4 GiB fp32, SLICE x WINDOW.  Each point builds its
 # own communicator (the knobs are read at ncclCommInitRank, as the reference's Config).
 SWEEP_POINTS = [
-    # (MINI_NCCL_CHANNELS, MINI_NCCL_THREADS, MINI_NCCL_SLICE_SIZE, algo, MINI_NCCL_SYS_FENCE)
-    (256, 64, 131072, "direct", 0), (64, 256, 131072, "direct", 0), (256, 128, 131072, "direct", 0),
-    (128, 64, 131072, "direct", 0), (256, 64, 524288, "direct", 0), (256, 64, 131072, "direct", 1),
-    (256, 64, 131072, "ring", 0), (64, 256, 131072, "ring", 0), (256, 128, 131072, "ring", 0),
-    (128, 64, 131072, "ring", 0), (256, 64, 524288, "ring", 0), (256, 64, 131072, "ring", 1),
+    # (algo, knobs over the library defaults: 256 one-wave workgroups, 128 KiB slices, 2 slots,
+    #  no hand-off fences, overlapped direct phases)
+    ("direct", {}), ("direct", {"MINI_NCCL_CHANNELS": 64, "MINI_NCCL_THREADS": 256}),
+    ("direct", {"MINI_NCCL_THREADS": 128}), ("direct", {"MINI_NCCL_CHANNELS": 512}),
+    ("direct", {"MINI_NCCL_SLOTS": 4}), ("direct", {"MINI_NCCL_SLICE_SIZE": 524288}),
+    ("direct", {"MINI_NCCL_SYS_FENCE": 1}), ("direct", {"MINI_NCCL_DIRECT_OVERLAP": 0}),
+    ("ring", {}), ("ring", {"MINI_NCCL_THREADS": 128}), ("ring", {"MINI_NCCL_SLOTS": 4}),
+    ("ring", {"MINI_NCCL_SLICE_SIZE": 524288}), ("ring", {"MINI_NCCL_SYS_FENCE": 1}),
 ]
 C4_SLICES = [65536, 131072, 262144, 1048576]
 C4_WINDOWS = [16, 32, 64]
@@ -190,11 +193,9 @@ def verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stre
 
 def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
     out = {"buffer": "256 MiB fp32", "points": []}
-    for ch, thr, sl, algo, fence in SWEEP_POINTS:
-        env = {"MINI_NCCL_CHANNELS": ch, "MINI_NCCL_THREADS": thr, "MINI_NCCL_SLICE_SIZE": sl,
-               "MINI_NCCL_SYS_FENCE": fence}
+    for algo, env in SWEEP_POINTS:
         r = sweep_point(M, torch, dist, dev, n, rank, env, algo, 64 << 20, 5, max_over_ranks)
-        out["points"].append({"algo": algo, "channels": ch, "threads": thr, "slice": sl, "sys_fence": fence, **r})
+        out["points"].append({"algo": algo, "env": {k[len("MINI_NCCL_"):].lower(): v for k, v in env.items()}, **r})
     if with_c4:  # BASELINE.json configs[3]: ring, 4 GiB fp32, SLICE x WINDOW
         c4 = []
         for w in C4_WINDOWS:
