@@ -105,6 +105,27 @@ def cpu_baseline(budget_s=10.0):
     }
 
 
+def cpu_ring_baseline(n, budget_s=4.0):
+    """N > 1 companion of cpu_baseline: the host ring, n threads of this box
+    (one per rank), the reference's schedule and operand order with AVX2 adds, on a bounded
+    sample (256 MiB fp32 per rank, not the 1 GiB of the GPU runs)."""
+    import ctypes
+
+    import numpy as np
+
+    import oracle_api as O
+    L = O.load()
+    cnt = (256 << 20) // 4
+    bufs = [np.ones(cnt, np.float32) for _ in range(n)]
+    arr = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+    t1 = L.oracle_cpu_ring_threads_avx2(arr, n, cnt, 131072, 1)  # also the first touch
+    iters = max(1, min(10, int(budget_s / max(t1, 1e-3))))
+    t = L.oracle_cpu_ring_threads_avx2(arr, n, cnt, 131072, iters)
+    return {"value": round(cnt * 4 / t / 1e9, 3), "unit": "GB/s", "cores": n, "kind": "port",
+            "sample": f"{n}-thread in-process host ring (reference schedule, AVX2 adds), 256 MiB fp32 per rank, "
+                      f"{iters} timed all-reduces after 1"}
+
+
 # ------------------------------------------------------------------ N > 1 configuration sweeps
 # (schedule, knob) points timed on a 256 MiB buffer, and the
 # BASELINE.json configs[3] (C4) grid: ring, 4 GiB fp32, SLICE x WINDOW.  Each point builds its
@@ -229,7 +250,7 @@ def pmc_traffic(key):
         return None, None
 
 
-EXTRAS_LIMIT_S = 300
+EXTRAS_LIMIT_S = float(os.environ.get("MNCCL_BENCH_EXTRAS_S", "300"))
 _emitted = []
 
 
@@ -271,6 +292,13 @@ def main():
             log("cpu baseline:", json.dumps(cpu))
         except Exception as e:
             log("cpu baseline failed:", e)
+
+    cpu_ring = None
+    if n > 1 and rank == 0 and not args.no_cpu_baseline:
+        try:
+            cpu_ring = cpu_ring_baseline(n)  # before the GPU is touched; the other ranks wait
+        except Exception as e:
+            cpu_ring = {"error": str(e)[:200]}
 
     import torch
     import mini_nccl as M
@@ -445,6 +473,8 @@ def main():
     # the extras below (RCCL's number, the sweeps) must never cost the headline line: if they
     # have not finished in EXTRAS_LIMIT_S, every rank gives up and rank 0 prints what it has
     result["cpu_baseline"] = cpu
+    if cpu_ring is not None:
+        result["cpu_ring_baseline"] = cpu_ring
     guard = None
     if n > 1:
         import threading
