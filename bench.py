@@ -254,11 +254,23 @@ EXTRAS_LIMIT_S = float(os.environ.get("MNCCL_BENCH_EXTRAS_S", "300"))
 _emitted = []
 
 
+_json_fd = [1]
+
+
+def quiet_stdout():
+    """Native libraries (gloo's connection banner, RCCL's version banner) print to fd 1: send
+    fd 1 to stderr for the whole run and keep the real stdout for the one JSON line."""
+    sys.stdout.flush()
+    _json_fd[0] = os.dup(1)
+    os.dup2(2, 1)
+
+
 def emit(result):
-    """print THE one JSON line (at most once)"""
+    """write THE one JSON line (at most once) to the real stdout"""
     if not _emitted:
         _emitted.append(True)
-        print(json.dumps(result), flush=True)
+        sys.stdout.flush()
+        os.write(_json_fd[0], (json.dumps(result) + "\n").encode())
 
 
 def main():
@@ -277,6 +289,7 @@ def main():
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on GPU 0 (as the reference's perf_test)")
     args = ap.parse_args()
+    quiet_stdout()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -530,7 +543,6 @@ if __name__ == "__main__":
         import traceback
         traceback.print_exc()
         if int(os.environ.get("RANK", "0")) == 0 and not _emitted:
-            print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "GB/s",
-                              "n_gpus": int(os.environ.get("WORLD_SIZE", "1")), "higher_is_better": True,
-                              "error": f"{type(e).__name__}: {e}"[:500]}), flush=True)
+            emit({"metric": METRIC, "value": 0.0, "unit": "GB/s", "n_gpus": int(os.environ.get("WORLD_SIZE", "1")),
+                  "higher_is_better": True, "error": f"{type(e).__name__}: {e}"[:500]})
         sys.exit(1)
