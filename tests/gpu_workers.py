@@ -81,16 +81,37 @@ def allreduce_rank(rank, n, port, cases, env, out_q):
                 recv.fill_byte(0xAB)
             rc = 0
             t0 = time.time()
+            bad, first, detail = 0, -1, ""
+            # "vary": new inputs every call, each call checked (a stale slot or flag from the
+            # previous call cannot pass); "skew_ms": each rank sleeps a random time before
+            # each call, so ranks enter every call out of step (injected-delay protocol test)
+            vary, skew = case.get("vary", False), case.get("skew_ms", 0)
+            rng = np.random.default_rng(seed * 97 + rank)
             for c in range(calls):
+                if vary and c > 0:
+                    xs = make_inputs(n, count, dtype, seed + 1000 * c, case.get("special", False))
+                    exp = O.allreduce(xs, dtype, op, inplace=inplace)[rank]
                 send.upload(xs[rank], off)
+                if skew:
+                    time.sleep(float(rng.uniform(0, skew)) / 1000.0)
                 rc = comm.all_reduce(send.ptr + off, recv.ptr + off, count, code, O.OPS[op], stream.handle)
                 if rc != 0:
                     break
+                if vary:
+                    stream.sync()
+                    got = recv.download(npd, count, off)
+                    b, f = compare(got, exp, dtype, op in ("sum", "prod"))
+                    if b and not bad:
+                        first, detail = f, f"call {c}: got {got[f]!r} expected {exp[f]!r}"
+                    bad += b
             stream.sync()
             dt = time.time() - t0
-            got = recv.download(npd, count, off)
-            bad, first = compare(got, exp, dtype, op in ("sum", "prod")) if rc == 0 else (-1, -1)
-            detail = (f"got {got[first]!r} expected {exp[first]!r}" if bad and first >= 0 else "")
+            if not vary:
+                got = recv.download(npd, count, off)
+                bad, first = compare(got, exp, dtype, op in ("sum", "prod")) if rc == 0 else (-1, -1)
+                detail = (f"got {got[first]!r} expected {exp[first]!r}" if bad and first >= 0 else "")
+            elif rc != 0:
+                bad, first = -1, -1
             results.append({"case": case, "rc": rc, "bad": bad, "first": first, "detail": detail, "secs": dt,
                             "async": comm.async_error()})
             send.free()

@@ -126,6 +126,18 @@ def test_host_buffers(dev, algo, stage_host):
 
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("blocking", ["1", "0"], ids=["blocking", "async"])
+def test_skewed_ranks_varying_data(dev, algo, blocking):
+    # injected delays (SURVEY.md §5 race detection): every rank sleeps 0-30 ms before each of
+    # 8 calls, inputs change every call and every call is checked; sizes alternate so the
+    # adaptive payload changes between calls while a peer may still drain the previous one
+    cases = [_case(count=c, algo=algo, calls=4, seed=40 + i, vary=True, skew_ms=30)
+             for i, c in enumerate(((1 << 20) + 3, 5000, (1 << 18) + 1))]
+    cases += [_case(dtype="bf16", count=300007, algo=algo, calls=4, seed=50, vary=True, skew_ms=30, inplace=True)]
+    _run_allreduce(4, cases, env={"MINI_NCCL_BLOCKING": blocking})
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
 def test_sys_fence_on(dev, algo):
     # MINI_NCCL_SYS_FENCE=1: system release / acquire fences around every hand-off (the
     # default relies on sc0 sc1 payload accesses of uncached scratch instead)
