@@ -53,8 +53,11 @@ def _build_abi_selftest(tmp_path):
 def _run_abi_selftest(exe, expect):
     import gpu_workers as GW
     env = {k: v for k, v in os.environ.items() if not k.startswith("MINI_NCCL_")}
-    # the HIP runtime keeps allocations until process exit: leak reports would be its own
-    env.update(MINI_NCCL_PORT=str(GW.free_port()), ASAN_OPTIONS="detect_leaks=0", UBSAN_OPTIONS="print_stacktrace=1")
+    # the HIP runtime keeps allocations until process exit (leak reports would be its own), and
+    # ASan cannot unmap its alternate signal stack in the runtime's threads (a CHECK failure in
+    # AsanThread::Destroy, seen on the MI355X box): no sigaltstack
+    env.update(MINI_NCCL_PORT=str(GW.free_port()), ASAN_OPTIONS="detect_leaks=0:use_sigaltstack=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
     p = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     assert expect in p.stdout
