@@ -91,7 +91,9 @@ def test_half_conversions_match_numpy(oracle_lib):
                        ).astype(np.float32)
     L = O.load()
     h = np.array([L.oracle_f32_to_f16(float(x)) for x in f], np.uint16)
-    assert np.array_equal(h, f.astype(np.float16).view(np.uint16))
+    with np.errstate(over="ignore"):  # values past 65520 round to inf on purpose
+        ref = f.astype(np.float16)
+    assert np.array_equal(h, ref.view(np.uint16))
     back = np.array([L.oracle_f16_to_f32(int(x)) for x in h[:5000]], np.float32)
     assert np.array_equal(back, h[:5000].view(np.float16).astype(np.float32))
     b = np.array([L.oracle_f32_to_bf16(float(x)) for x in f[:5000]], np.uint16)
