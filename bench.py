@@ -146,6 +146,7 @@ C4_WINDOWS = [16, 32, 64]
 
 def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_ranks):
     """one communicator with `env` knobs; returns algbw GB/s (max time over ranks) and check"""
+    env = dict(env, MINI_NCCL_TUNE=0)  # the point sets its schedule itself
     saved = {k: os.environ.get(k) for k in env}
     os.environ.update({k: str(v) for k, v in env.items()})
     comm = None
@@ -445,7 +446,8 @@ def main():
                                    f"HIP IPC over xGMI, {args.algo} schedule",
                        "count": count, "bytes": nbytes, "algo": args.algo, "slice_bytes": info["slice_bytes"],
                        "channels": info["channels"], "slots": info["slots"], "threads": info["threads"],
-                       "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED"},
+                       "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
+                       "auto_tune_ms": {"ring": round(info["tune_ms"][0], 4), "direct": round(info["tune_ms"][1], 4)}},
             "busbw": round(algbw * 2 * (n - 1) / n, 3),
         })
         # ceiling of each schedule from the probed links (min over ranks): ring moves

@@ -29,7 +29,8 @@ typedef enum {
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
   mncclAlgoDirect = 1  /* every peer pushes its slice of chunk c straight to rank c over its
                           own xGMI link; c folds them in ring order c, c+1, ..., c-1 and
-                          pushes the result to every peer (default from 3 ranks on) */
+                          pushes the result to every peer (from 3 ranks on, MINI_NCCL_ALGO=auto
+                          times both at init and keeps the faster) */
 } mncclAlgo_t;
 
 typedef struct {
@@ -45,6 +46,9 @@ typedef struct {
   int sys_fence;          /* MINI_NCCL_SYS_FENCE: system-scope release fence before each flag */
   double timeout_s;       /* MINI_NCCL_TIMEOUT_MS / 1000 */
   size_t scratch_bytes;   /* device scratch owned by this rank */
+  double tune_ms[2];      /* MINI_NCCL_ALGO=auto calibration at init (3+ ranks): ms per
+                             all-reduce of MINI_NCCL_TUNE_BYTES, ring / direct, max over
+                             ranks; 0 when not run (algo forced, MINI_NCCL_TUNE=0, 2 ranks) */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,

@@ -156,6 +156,8 @@ ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info) {
   info->sys_fence = k.sys_fence;
   info->timeout_s = k.timeout_ms / 1000.0;
   info->scratch_bytes = c->scratch_bytes();
+  info->tune_ms[0] = c->tune_ms(0);
+  info->tune_ms[1] = c->tune_ms(1);
   return ncclSuccess;
 }
 

@@ -5,6 +5,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -61,6 +62,7 @@ Comm::Comm(int nranks, int rank, const std::string& ip) : rank_(rank), nranks_(n
     setup_device_resources();
     boot_.connect(rank, nranks, ip, cfg_.port, cfg_.bootstrap_timeout_ms / 1000.0);
     exchange_and_map();
+    if (cfg_.algo < 0 && cfg_.tune && nranks >= 3) tune();
   } catch (...) {
     release();
     throw;
@@ -160,6 +162,56 @@ void Comm::exchange_and_map() {
   }
   // every rank has mapped every peer and its own memory is zeroed before anyone writes
   boot_.barrier();
+}
+
+// MINI_NCCL_ALGO=auto from 3 ranks on: both schedules give the same bits, and which one is
+// faster depends on the links (on the xGMI mesh `direct` spreads over n-1 links, on a shared
+// device the ring's fewer bytes per hop can win).  Time one in-place all-reduce of
+// MINI_NCCL_TUNE_BYTES per rank with each (one warm-up, three timed), take the max over ranks
+// (allgather over the bootstrap, so every rank computes the same choice) and keep the faster.
+void Comm::tune() {
+  const size_t count = cfg_.tune_bytes / 4;
+  float* buf = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  double ms[2] = {0.0, 0.0};
+  bool ok = true;
+  try {
+    hip_check(hipMalloc((void**)&buf, count * 4), "tune alloc");
+    hip_check(hipMemset(buf, 0, count * 4), "tune memset");
+    hip_check(hipDeviceSynchronize(), "tune sync");
+    hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "tune stream");
+    hip_check(hipEventCreate(&e0), "tune event");
+    hip_check(hipEventCreate(&e1), "tune event");
+    for (int a = 0; a < 2 && ok; ++a) {
+      algo_ = a;
+      ok = allreduce(buf, buf, count, kF32, kSum, st) == ncclSuccess;
+      hip_check(hipStreamSynchronize(st), "tune sync");
+      boot_.barrier();
+      hip_check(hipEventRecord(e0, st), "tune event");
+      for (int i = 0; i < 3 && ok; ++i) ok = allreduce(buf, buf, count, kF32, kSum, st) == ncclSuccess;
+      hip_check(hipEventRecord(e1, st), "tune event");
+      hip_check(hipEventSynchronize(e1), "tune wait");
+      float t = 0.f;
+      hip_check(hipEventElapsedTime(&t, e0, e1), "tune time");
+      ms[a] = t / 3.0;
+    }
+  } catch (...) {
+    ok = false;
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  if (st) hipStreamDestroy(st);
+  if (buf) hipFree(buf);
+  if (!ok || sticky_ != ncclSuccess) throw std::runtime_error("auto-tune all-reduce failed");
+  std::vector<double> all((size_t)nranks_ * 2);
+  boot_.allgather(ms, all.data(), sizeof ms);
+  for (int q = 0; q < nranks_; ++q)
+    for (int a = 0; a < 2; ++a) tune_ms_[a] = std::max(tune_ms_[a], all[(size_t)q * 2 + a]);
+  algo_ = tune_ms_[1] <= tune_ms_[0] ? 1 : 0;
+  if (cfg_.debug && rank_ == 0)
+    fprintf(stderr, "[Mini-NCCL] auto-tune %zu B: ring %.3f ms, direct %.3f ms -> %s\n", count * 4, tune_ms_[0],
+            tune_ms_[1], algo_ ? "direct" : "ring");
 }
 
 Comm::~Comm() {

@@ -32,6 +32,8 @@ class Comm {
   const Config& config() const { return cfg_; }
   int algo() const { return algo_; }
   void set_algo(int a) { algo_ = a; }
+  // calibration of MINI_NCCL_ALGO=auto (max over ranks, ms per call; 0 = not run)
+  double tune_ms(int a) const { return tune_ms_[a & 1]; }
   ncclResult_t async_error();
   // Collective: every rank writes `bytes` into the next rank's scratch (all_peers = 0) or into
   // every peer's scratch at once (1), `iters` times; *gbps = bytes per second per link
@@ -46,6 +48,7 @@ class Comm {
   void setup_device_resources();
   void release();
   void exchange_and_map();
+  void tune();
   ncclResult_t wait_for(hipStream_t stream);
   enum class Reach { kDevice, kMapped, kStaged };
   Reach reach(const void* p, const void** kernel_ptr) const;
@@ -56,6 +59,7 @@ class Comm {
   int rank_, nranks_, device_ = 0;
   Config cfg_;
   int algo_ = 0;
+  double tune_ms_[2] = {0.0, 0.0};
   Bootstrap boot_;
 
   char* scratch_ = nullptr;      // uncached device memory, peers write into it

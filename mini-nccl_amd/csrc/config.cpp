@@ -65,6 +65,10 @@ Config Config::from_env() {
   c.pipe_depth = (int)env_int("MINI_NCCL_PIPE_DEPTH", 1);
   if (c.pipe_depth < 1) c.pipe_depth = 1;
   c.direct_overlap = env_int("MINI_NCCL_DIRECT_OVERLAP", 1) != 0;
+  c.tune = env_int("MINI_NCCL_TUNE", 1) != 0;
+  long long tb = env_int("MINI_NCCL_TUNE_BYTES", 64LL << 20);
+  if (tb < (1LL << 20)) tb = 1LL << 20;
+  c.tune_bytes = (size_t)(tb & ~255LL);
   c.stage_host = env_int("MINI_NCCL_STAGE_HOST", 0) != 0;
   c.timeout_ms = (double)env_int("MINI_NCCL_TIMEOUT_MS", 10000);
   if (c.timeout_ms < 1) c.timeout_ms = 1;
@@ -78,10 +82,10 @@ std::string Config::describe() const {
   char b[320];
   snprintf(b, sizeof b,
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, algo=%s, blocking=%d, "
-           "sys_fence=%d, min_slice=%zu, depth=%d, stage_host=%d, timeout=%.0f ms, port=%d",
+           "sys_fence=%d, min_slice=%zu, depth=%d, tune=%d, stage_host=%d, timeout=%.0f ms, port=%d",
            slice_size, window_size, signal_batch, slots, channels, threads,
            algo < 0 ? "auto" : algo ? "direct" : "ring", blocking,
-           sys_fence, min_slice, pipe_depth, stage_host, timeout_ms, port);
+           sys_fence, min_slice, pipe_depth, tune, stage_host, timeout_ms, port);
   return b;
 }
 

@@ -22,6 +22,8 @@ struct Config {
   size_t min_slice = 1024;         // MINI_NCCL_MIN_SLICE smallest adaptive payload (>= SLICE_SIZE: adaptation off)
   int pipe_depth = 1;              // MINI_NCCL_PIPE_DEPTH slices per pipeline targeted for small calls
   int direct_overlap = 1;          // MINI_NCCL_DIRECT_OVERLAP next iteration's raw pushes before this one's results
+  int tune = 1;                    // MINI_NCCL_TUNE   auto algo: time both schedules at init (n >= 3)
+  size_t tune_bytes = 64u << 20;   // MINI_NCCL_TUNE_BYTES per-rank buffer of that calibration
   int stage_host = 0;              // MINI_NCCL_STAGE_HOST pinned host buffers: 0 = kernel maps them, 1 = staged copy
   double timeout_ms = 10000.0;     // MINI_NCCL_TIMEOUT_MS (reference watchdog: 10 s)
   int port = 8888;                 // MINI_NCCL_PORT   bootstrap port (reference: 8888)

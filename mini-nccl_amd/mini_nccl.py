@@ -47,7 +47,7 @@ class CommInfo(ctypes.Structure):
         ("slice_bytes", ctypes.c_size_t), ("window", ctypes.c_int), ("signal_batch", ctypes.c_int),
         ("channels", ctypes.c_int), ("slots", ctypes.c_int), ("threads", ctypes.c_int),
         ("algo", ctypes.c_int), ("blocking", ctypes.c_int), ("sys_fence", ctypes.c_int),
-        ("timeout_s", ctypes.c_double), ("scratch_bytes", ctypes.c_size_t),
+        ("timeout_s", ctypes.c_double), ("scratch_bytes", ctypes.c_size_t), ("tune_ms", ctypes.c_double * 2),
     ]
 
 
@@ -129,7 +129,9 @@ class Comm:
     def info(self):
         i = CommInfo()
         check(load().mncclCommGetInfo(self.handle, ctypes.byref(i)))
-        return {f: getattr(i, f) for f, _ in CommInfo._fields_}
+        d = {f: getattr(i, f) for f, _ in CommInfo._fields_}
+        d["tune_ms"] = list(d["tune_ms"])
+        return d
 
     def link_probe(self, all_peers=False, nbytes=0, iters=10):
         """GB/s per destination link (collective: every rank must call it)."""

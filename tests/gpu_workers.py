@@ -215,6 +215,21 @@ def init_rank(rank, n, port, env, out_q):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def info_rank(rank, n, port, env, out_q):
+    """Create a communicator with `env`, report mncclCommGetInfo, destroy it."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        hip_rt.set_device(0)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        info = comm.info()
+        out_q.put((rank, {"info": info, "destroy": comm.destroy()}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
 def huge_rank(rank, n, port, env, count, out_q):
     """64-bit element counts (the reference narrowed count to int, mini_nccl.h:113): bf16
     all-ones in place -> body == n, tail == 1 (size-independent known answer)."""

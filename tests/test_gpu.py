@@ -71,7 +71,8 @@ def test_local_reduce_in_place_large(dev):
 
 def _run_allreduce(n, cases, env=None, timeout=300):
     port = GW.free_port()
-    e = {"MINI_NCCL_TIMEOUT_MS": "30000"}
+    # every case sets its schedule explicitly: no auto-tune run at init
+    e = {"MINI_NCCL_TIMEOUT_MS": "30000", "MINI_NCCL_TUNE": "0"}
     e.update(env or {})
     out = GW.run_ranks(GW.allreduce_rank, n, lambda r: (r, n, port, cases, e), timeout)
     assert len(out) == n, f"only ranks {sorted(out)} reported (timeout?)"
@@ -135,6 +136,22 @@ def test_skewed_ranks_varying_data(dev, algo, blocking):
              for i, c in enumerate(((1 << 20) + 3, 5000, (1 << 18) + 1))]
     cases += [_case(dtype="bf16", count=300007, algo=algo, calls=4, seed=50, vary=True, skew_ms=30, inplace=True)]
     _run_allreduce(4, cases, env={"MINI_NCCL_BLOCKING": blocking})
+
+
+def test_auto_tune_picks_the_faster_schedule(dev):
+    # MINI_NCCL_ALGO=auto from 3 ranks: both schedules timed at init (max over ranks, every rank
+    # sees the same numbers), the faster kept; forcing a schedule or 2 ranks skips it
+    port = GW.free_port()
+    env = {"MINI_NCCL_TUNE_BYTES": str(8 << 20)}
+    out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, env), 120)
+    assert all("error" not in out[r] for r in range(3)), out
+    infos = [out[r]["info"] for r in range(3)]
+    t = infos[0]["tune_ms"]
+    assert t[0] > 0 and t[1] > 0 and all(i["tune_ms"] == t for i in infos)
+    assert all(i["algo"] == (1 if t[1] <= t[0] else 0) for i in infos)
+    port = GW.free_port()
+    out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {"MINI_NCCL_ALGO": "direct"}), 120)
+    assert out[0]["info"]["tune_ms"] == [0.0, 0.0] and out[0]["info"]["algo"] == 1
 
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
