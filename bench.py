@@ -137,11 +137,15 @@ SWEEP_POINTS = [
     ("direct", {"MINI_NCCL_THREADS": 128}), ("direct", {"MINI_NCCL_CHANNELS": 512}),
     ("direct", {"MINI_NCCL_SLOTS": 4}), ("direct", {"MINI_NCCL_SLICE_SIZE": 524288}),
     ("direct", {"MINI_NCCL_SYS_FENCE": 1}), ("direct", {"MINI_NCCL_DIRECT_OVERLAP": 0}),
+    ("direct", {"MINI_NCCL_SLICE_SIZE": 32768}), ("direct", {"MINI_NCCL_SLICE_SIZE": 65536}),
+    ("direct", {"MINI_NCCL_CHANNELS": 128}),
     ("ring", {}), ("ring", {"MINI_NCCL_THREADS": 128}), ("ring", {"MINI_NCCL_SLOTS": 4}),
     ("ring", {"MINI_NCCL_SLICE_SIZE": 524288}), ("ring", {"MINI_NCCL_SYS_FENCE": 1}),
 ]
 C4_SLICES = [65536, 131072, 262144, 1048576]
 C4_WINDOWS = [16, 32, 64]
+# 4 GiB fp32 per rank; MNCCL_BENCH_C4_MIB / MNCCL_BENCH_C4=1 rehearse the grid smaller / at n < 8
+C4_COUNT = int(os.environ.get("MNCCL_BENCH_C4_MIB", "4096")) * (1 << 20) // 4
 
 
 def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_ranks):
@@ -219,14 +223,63 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
         r = sweep_point(M, torch, dist, dev, n, rank, env, algo, 64 << 20, 5, max_over_ranks)
         out["points"].append({"algo": algo, "env": {k[len("MINI_NCCL_"):].lower(): v for k, v in env.items()}, **r})
     if with_c4:  # BASELINE.json configs[3]: ring, 4 GiB fp32, SLICE x WINDOW
+        out["c4_buffer_MiB"] = C4_COUNT * 4 >> 20
         c4 = []
         for w in C4_WINDOWS:
             for sl in C4_SLICES:
                 env = {"MINI_NCCL_WINDOW_SIZE": w, "MINI_NCCL_SLICE_SIZE": sl}
-                r = sweep_point(M, torch, dist, dev, n, rank, env, "ring", 1 << 30, 3, max_over_ranks)
+                r = sweep_point(M, torch, dist, dev, n, rank, env, "ring", C4_COUNT, 3, max_over_ranks)
                 c4.append({"window": w, "slice": sl, **r})
         out["c4_ring_4GiB"] = c4
     return out
+
+
+PERF_TEST_MIB = [1, 16, 64, 128]  # tests/perf_test.cpp:69
+
+
+def size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks, warm=5, reps=20):
+    """algbw of this library (default schedule) and of RCCL at the reference perf_test's sizes"""
+    rows = []
+    for mib in PERF_TEST_MIB:
+        k = (mib << 20) // 4
+        if k > send.numel():
+            break
+        s_, r_ = send[:k], recv[:k]
+
+        def ours():
+            rc = comm.all_reduce(s_.data_ptr(), r_.data_ptr(), k, M.ncclFloat, M.ncclSum, stream.cuda_stream)
+            if rc != 0:
+                raise M.NcclError(rc, "ncclAllReduce")
+
+        row = {"MiB": mib}
+        for name, fn in (("mini_nccl", ours), ("rccl", None if pg is None else
+                                                  (lambda: torch.distributed.all_reduce(r_, group=pg)))):
+            if fn is None:
+                continue
+            try:
+                for _ in range(warm):
+                    fn()
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    fn()
+                torch.cuda.synchronize()
+                dt = max_over_ranks(time.perf_counter() - t0) / reps
+                row[name + "_us"] = round(dt * 1e6, 1)
+                row[name + "_algbw_GBps"] = round(k * 4 / dt / 1e9, 2)
+            except Exception as e:
+                if name == "mini_nccl":
+                    raise
+                pg = None  # RCCL refused (e.g. two ranks on one GPU): skip it from here on
+                row["rccl_error"] = str(e)[:80]
+                dist.barrier()
+        ok = comm.async_error() == 0
+        ours()
+        torch.cuda.synchronize()
+        row["ok"] = max_over_ranks(0.0 if (ok and bool((r_ == float(n)).all().item())) else 1.0) == 0.0
+        rows.append(row)
+    return rows
 
 
 # ------------------------------------------------------------------ helpers
@@ -511,6 +564,42 @@ def main():
         fa = fused / (ev_ms / 1e3) / 1e9
         result["roofline"].update({"fused_alg_bytes_per_launch": fused, "fused_achieved": round(fa, 2),
                                    "fused_frac": round(fa / HBM_PEAK_GBS, 4)})
+        # the north star's "scatter-reduce sum kernel" on its own, on THIS GPU: one launch of the
+        # element-wise op over the (n-1) * chunk elements a rank reduces per call (SURVEY §8d's
+        # bytes exactly), HIP events around each launch; inside the fused kernel the same adds
+        # run at the links' pace ("The >= 70 % target")
+        m = (n - 1) * (count // n)
+        sk_ms, sk_err = 0.0, None
+        # on a real node every rank has its own GPU; ranks sharing one GPU take turns
+        for turn in (range(n) if args.same_device else [rank]):
+            if args.same_device:
+                dist.barrier()
+            if turn != rank:
+                continue
+            try:
+                sh_ = stream.cuda_stream
+                ks = []
+                for i in range(25):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    rc = M.local_reduce(recv.data_ptr(), recv.data_ptr(), send.data_ptr(), m, ndt, M.ncclSum, sh_)
+                    e1.record(stream)
+                    if rc != 0:
+                        raise M.NcclError(rc, "mncclLocalReduce")
+                    if i >= 5:
+                        ks.append((e0, e1))
+                torch.cuda.synchronize()
+                sk_ms = sum(a.elapsed_time(b) for a, b in ks) / len(ks)
+            except Exception as e:
+                sk_ms, sk_err = float("inf"), str(e)[:200]
+        sk_ms = max_over_ranks(sk_ms)  # every rank gets here, failed or not
+        if sk_err is None and sk_ms != float("inf"):
+            sk = 3 * esz * m / (sk_ms / 1e3) / 1e9
+            result["roofline"]["sum_kernel"] = {"kernel": "local_reduce_vec", "elements": m, "alg_bytes": 3 * esz * m,
+                                                "kernel_ms": round(sk_ms, 4), "achieved": round(sk, 2),
+                                                "frac": round(sk / HBM_PEAK_GBS, 4)}
+        else:
+            result["roofline"]["sum_kernel"] = {"error": sk_err or "failed on another rank"}
     # the extras below (RCCL's number, the sweeps) must never cost the headline line: if they
     # have not finished in EXTRAS_LIMIT_S, every rank gives up and rank 0 prints what it has
     result["cpu_baseline"] = cpu
@@ -532,6 +621,7 @@ def main():
         guard.start()
     if n > 1 and not args.no_alt:
         # the comparison ceiling: RCCL's all-reduce on the same buffer (torch.distributed nccl)
+        pg = None
         try:
             import torch.distributed as dist_
             pg = dist_.new_group(backend="nccl")
@@ -548,8 +638,19 @@ def main():
             w3 = max_over_ranks(time.perf_counter() - t0)
             result["rccl_reference"] = {"value": round(nbytes / (w3 / args.steps) / 1e9, 3),
                                         "ms_per_step": round(w3 / args.steps * 1e3, 4)}
+            del x
         except Exception as e:
             result["rccl_reference"] = {"error": str(e)[:200]}
+            pg = None
+        if rank == 0:
+            arm(result)
+        # the reference's perf_test sizes (perf_test.cpp:69: 1/16/64/128 MiB), this library's
+        # default schedule next to RCCL's all-reduce, device-resident fp32
+        try:
+            if args.dtype == "f32":
+                result["sizes"] = size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks)
+        except Exception as e:
+            result["sizes"] = {"error": str(e)[:200]}
         if rank == 0:
             arm(result)
     if n > 1:
@@ -558,7 +659,7 @@ def main():
         torch.cuda.empty_cache()
         if not args.no_sweep and args.dtype == "f32":
             t_sw = time.time()
-            result["sweep"] = run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4=(n == 8))
+            result["sweep"] = run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4=(n == 8 or os.environ.get("MNCCL_BENCH_C4") == "1"))
             result["sweep"]["wall_s"] = round(time.time() - t_sw, 1)
     if guard is not None:
         guard.cancel()
