@@ -85,6 +85,35 @@ __global__ void __launch_bounds__(64) lds_dma(v4f* out, const v4f* a, const v4f*
   __builtin_nontemporal_store(x + tile[threadIdx.x], out + i);
 }
 
+// XCD-aware block order: workgroups are dealt round-robin to the 8 XCDs (b % 8); remap so
+// XCD x walks contiguous runs of G KiB-blocks instead of every 8th KiB
+template <int G>
+__global__ void __launch_bounds__(64) xcd_remap(v4f* out, const v4f* a, const v4f* b, size_t nvec) {
+  const size_t nblk = gridDim.x;  // multiple of 8 * G (caller)
+  const size_t bx = blockIdx.x, x = bx & 7, k = bx >> 3;  // k-th block of XCD x
+  const size_t per = nblk / 8;
+  const size_t lb = (G == 0) ? x * per + k : ((k / G) * 8 + x) * G + (k % G);
+  const size_t i = lb * 64 + threadIdx.x;
+  const v4f p = __builtin_nontemporal_load(a + i);
+  const v4f q = __builtin_nontemporal_load(b + i);
+  __builtin_nontemporal_store(p + q, out + i);
+}
+// cache-policy bits on buffer ops (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16)
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+template <int LA, int SA>
+__global__ void __launch_bounds__(64) pol(v4f* out, const v4f* a, const v4f* b, size_t nvec) {
+  const size_t i = blockIdx.x * 64 + threadIdx.x;
+  const size_t base = (size_t)blockIdx.x * 1024;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)a + base), (short)0, 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)b + base), (short)0, 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)out + base), (short)0, 1024, 0x00020000);
+  (void)i;
+  v4u p = __builtin_amdgcn_raw_buffer_load_b128(ra, threadIdx.x * 16, 0, LA);
+  v4u q = __builtin_amdgcn_raw_buffer_load_b128(rb, threadIdx.x * 16, 0, LA);
+  v4f r = __builtin_bit_cast(v4f, p) + __builtin_bit_cast(v4f, q);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, r), ro, threadIdx.x * 16, 0, SA);
+}
+
 struct Var { const char* name; void (*launch)(v4f*, const v4f*, const v4f*, size_t); };
 
 template <int U, int NTL, int NTS, int NT, int GRID>
@@ -95,6 +124,10 @@ template <int U, int NT>
 void Lcontig(v4f* o, const v4f* a, const v4f* b, size_t n) { contig<U><<<(unsigned)((n + (size_t)NT * U - 1) / ((size_t)NT * U)), NT>>>(o, a, b, n); }
 void Llds_reg(v4f* o, const v4f* a, const v4f* b, size_t n) { lds_reg<<<(unsigned)((n + 63) / 64), 64>>>(o, a, b, n); }
 void Llds_dma(v4f* o, const v4f* a, const v4f* b, size_t n) { lds_dma<<<(unsigned)(n / 64), 64>>>(o, a, b, n); }
+template <int G>
+void Lxcd(v4f* o, const v4f* a, const v4f* b, size_t n) { xcd_remap<G><<<(unsigned)(n / 64), 64>>>(o, a, b, n); }
+template <int LA, int SA>
+void Lpol(v4f* o, const v4f* a, const v4f* b, size_t n) { pol<LA, SA><<<(unsigned)(n / 64), 64>>>(o, a, b, n); }
 template <int U, int NTL, int NTS, int NT, int GRID>
 void Lnc(v4f* o, const v4f* a, const v4f* b, size_t n) { gs_nochk<U, NTL, NTS><<<GRID, NT>>>(o, a, b, n); }
 
@@ -106,15 +139,17 @@ int main() {
   CK(hipMemset(a, 0, count * 4));
   CK(hipMemset(b, 0, count * 4));
   std::vector<Var> vs = {
-    {"U4 nt/nt 256x4096 grid-stride", L<4, 1, 1, 256, 4096>},
-    {"U4 pl/pl 256x4096 grid-stride", L<4, 0, 0, 256, 4096>},
     {"U1 nt/nt 64 exact (shipped)", Lexact<1, 1, 1, 64>},
+    {"XCD remap: 8 contiguous regions", Lxcd<0>},
+    {"XCD remap: runs of 4 KiB", Lxcd<4>},
+    {"XCD remap: runs of 64 KiB", Lxcd<64>},
+    {"XCD remap: runs of 1 MiB", Lxcd<1024>},
+    {"buffer ld nt / st nt", Lpol<2, 2>},
+    {"buffer ld nt / st nt|sc1", Lpol<2, 18>},
+    {"buffer ld nt / st sc0|sc1", Lpol<2, 17>},
+    {"buffer ld 0 / st nt", Lpol<0, 2>},
+    {"buffer ld nt|sc1 / st nt", Lpol<18, 2>},
     {"U1 nt/nt 128 exact", Lexact<1, 1, 1, 128>},
-    {"U1 nt/nt 256 exact", Lexact<1, 1, 1, 256>},
-    {"U2 nt/nt 64 exact", Lexact<2, 1, 1, 64>},
-    {"U1 pl/pl 64 exact", Lexact<1, 0, 0, 64>},
-    {"LDS-staged b (registers) 64", Llds_reg},
-    {"LDS-staged b (LDS-DMA) 64", Llds_dma},
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
