@@ -241,22 +241,22 @@ __device__ __forceinline__ void move_scalar(const char* __restrict__ lsrc, char*
 // 16-byte vectors over the message, then its last (nbytes % 16) bytes element by element.
 // The local side (send / recv) may be element- but not 16-byte-aligned (4-byte-aligned
 // dwordx4 accesses are valid on gfx950); the slot side is always 16-byte-aligned.
-template <typename T, int OPC, int KIND>
+template <typename T, int OPC, int KIND, int UB = kU>
 __device__ __forceinline__ void move_vec(const char* __restrict__ lsrc, char* __restrict__ ldst, rsrc_t in,
                                          rsrc_t out, uint32_t nbytes, int lane) {
   constexpr int B = KindBits<KIND>::v;
   const uint32_t nvec = nbytes >> 4;
   uint32_t b = 0;
-  for (; b + 64 * kU <= nvec; b += 64 * kU) {  // full batches: every lane issues kU loads per stream
-    v4u l[kU], x[kU];
+  for (; b + 64 * UB <= nvec; b += 64 * UB) {  // full batches: every lane issues UB loads per stream
+    v4u l[UB], x[UB];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < UB; ++u) {
       const uint32_t i = b + (uint32_t)(u * 64 + lane);
       if (B & kHasLocal) l[u] = ld_g16(lsrc + (size_t)i * 16);
       if (B & kHasIn) x[u] = ld_slot16(in, i * 16);
     }
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < UB; ++u) {
       const uint32_t i = b + (uint32_t)(u * 64 + lane);
       v4u v;
       if (B & kReduces) v = reduce16<T, OPC>(l[u], x[u]);
@@ -289,9 +289,9 @@ __device__ __forceinline__ void move_scalar(const char* __restrict__ lsrc, char*
   }
 }
 
-template <typename T, int OPC, bool VEC, int KIND>
+template <typename T, int OPC, bool VEC, int KIND, int UB = kU>
 __device__ __forceinline__ void move(const char* lsrc, char* ldst, rsrc_t in, rsrc_t out, uint32_t nbytes, int lane) {
-  if (VEC) move_vec<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, lane);
+  if (VEC) move_vec<T, OPC, KIND, UB>(lsrc, ldst, in, out, nbytes, lane);
   else move_scalar<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, lane, 0);
 }
 
@@ -473,6 +473,16 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
 
 constexpr int kMaxWaves = 16;
 
+// Phase A's raw pushes are pure remote stores.  One vmcnt counts loads and stores in issue
+// order, so a batch's loads cannot be used before the previous batch's stores are acknowledged
+// -- over xGMI, a remote round trip: a wave keeps at most one batch of remote stores in
+// flight.  Twice the moves' batch (16 KiB per wave) doubles that for the one phase with no
+// other outbound stream (phase B already pushes n-1 batches per fold batch).
+#ifndef MNCCL_PUSH_U
+#define MNCCL_PUSH_U 16
+#endif
+constexpr int kPushU = MNCCL_PUSH_U;
+
 template <typename T, int OPC, bool VEC>
 __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
   const WaveId id = wave_id();
@@ -521,7 +531,7 @@ __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
         if (len) {
           const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, seq0), len);
           const u64 coff = (u64)d * p.chunk_bytes + soff;
-          move<T, OPC, VEC, kSend>(p.send + coff, nullptr, out, out, len, lane);
+          move<T, OPC, VEC, kSend, kPushU>(p.send + coff, nullptr, out, out, len, lane);
         }
       }
       drain_stores();
