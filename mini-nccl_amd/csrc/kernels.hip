@@ -63,14 +63,13 @@ template <> struct Op<int32_t, kSum> {
 template <> struct Op<int32_t, kProd> {
   __device__ static int32_t f(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
 };
-// bf16: widen (exact), op in f32, round to nearest even (correctly rounded: 24 >= 2*8+2);
-// NaN -> quiet NaN keeping the high payload bits (same rule as the oracle)
+// bf16: widen (exact), op in f32, round to nearest even (correctly rounded: 24 >= 2*8+2) with
+// the hardware's v_cvt_pk_bf16_f32 (gfx950; the compiler pairs two elements per instruction);
+// NaN stays NaN (its payload is the hardware's, as IEEE leaves it to the implementation)
 __device__ __forceinline__ float bf2f(bf16_t x) { return __uint_as_float((uint32_t)x.v << 16); }
 __device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
   bf16_t r;
-  if ((u & 0x7fffffffu) > 0x7f800000u) r.v = (uint16_t)((u >> 16) | 0x40u);
-  else r.v = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  r.v = __builtin_bit_cast(uint16_t, (__bf16)f);
   return r;
 }
 template <> struct Op<bf16_t, kSum> { __device__ static bf16_t f(bf16_t a, bf16_t b) { return f2bf(bf2f(a) + bf2f(b)); } };
