@@ -1,9 +1,10 @@
 #!/bin/bash
 # rocprofv3 evidence for the all-reduce kernels on ONE GPU (ranks sharing it; the 8-GPU run is
 # the driver's): rank 0 of apps/bin/perf_test under the profiler, the other ranks plain.
-#   1) --kernel-trace --stats, 2 ranks (ring, the default) and 4 ranks (direct, the default)
-#   2) --pmc FETCH_SIZE, 3) --pmc WRITE_SIZE (separate passes), 2 ranks.  TCC counters are
-#      device-wide: with both ranks' kernels resident they count BOTH ranks' traffic.
+#   1) --kernel-trace --stats, 2 ranks (ring, the default) and 4 ranks (auto-tuned at init)
+#   2) --pmc FETCH_SIZE, 3) --pmc WRITE_SIZE (separate passes), 2 ranks.  The counts come out
+#      at ONE rank's bytes (1.007 x): the other rank process's concurrent kernel is not in them.
+# Summaries: tools/proxy_stats.py <tag> <round>, tools/proxy_pmc.py <tag> <round>.
 set -o pipefail
 TAG=${1:-prof_proxy}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
