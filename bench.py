@@ -282,6 +282,37 @@ def size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks, 
     return rows
 
 
+def host_buffer_rate(M, torch, dist, comm, stream, n, max_over_ranks, mib=256, warm=2, reps=5):
+    """algbw of ncclAllReduce on pinned host send/recv buffers (never the headline value)"""
+    err = None
+    try:
+        k = (mib << 20) // 4
+        hs = torch.ones(k, dtype=torch.float32).pin_memory()
+        hr = torch.empty(k, dtype=torch.float32).pin_memory()
+
+        def call():
+            rc = comm.all_reduce(hs.data_ptr(), hr.data_ptr(), k, M.ncclFloat, M.ncclSum, stream.cuda_stream)
+            if rc != 0:
+                raise M.NcclError(rc, "ncclAllReduce (host buffers)")
+
+        for _ in range(warm):
+            call()
+        torch.cuda.synchronize()
+    except Exception as e:
+        err = str(e)[:160]
+    if max_over_ranks(1.0 if err else 0.0) != 0.0:  # every rank agrees before timing
+        return {"error": err or "failed on another rank"}
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        call()
+    torch.cuda.synchronize()
+    dt = max_over_ranks(time.perf_counter() - t0) / reps
+    ok = max_over_ranks(0.0 if bool((hr == float(n)).all().item()) else 1.0) == 0.0
+    return {"buffer": f"{mib} MiB fp32 pinned host memory (send and recv), mapped into the kernel",
+            "algbw_GBps": round(k * 4 / dt / 1e9, 2), "ms": round(dt * 1e3, 3), "ok": ok}
+
+
 # ------------------------------------------------------------------ helpers
 def reduce_max(dist, x):
     """max over ranks of a host scalar through the harness's (gloo) process group"""
@@ -653,6 +684,12 @@ def main():
             result["sizes"] = {"error": str(e)[:200]}
         if rank == 0:
             arm(result)
+        # the reference's own usage: host buffers in, host buffers out (perf_test.cpp:78-79);
+        # pinned memory is mapped into the kernel, so this is the PCIe-inclusive end-to-end rate
+        if args.dtype == "f32":
+            result["host_buffers"] = host_buffer_rate(M, torch, dist, comm, stream, n, max_over_ranks)
+            if rank == 0:
+                arm(result)
     if n > 1:
         comm.destroy()
         del send, recv
