@@ -473,10 +473,10 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
 constexpr int kMaxWaves = 16;
 
 // Phase A's raw pushes are pure remote stores.  One vmcnt counts loads and stores in issue
-// order, so a batch's loads cannot be used before the previous batch's stores are acknowledged
-// -- over xGMI, a remote round trip: a wave keeps at most one batch of remote stores in
-// flight.  Twice the moves' batch (16 KiB per wave) doubles that for the one phase with no
-// other outbound stream (phase B already pushes n-1 batches per fold batch).
+// order, so a batch's loads cannot be used before the previous batch's stores are acknowledged:
+// a wave keeps one batch of stores in flight.  Twice the moves' batch (16 KiB per wave) for the
+// one phase with no other outbound stream (phase B pushes n-1 batches per fold batch): +17 %
+// per wave into far memory (tools/far_store_probe.hip).
 #ifndef MNCCL_PUSH_U
 #define MNCCL_PUSH_U 16
 #endif
