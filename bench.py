@@ -44,7 +44,7 @@ def log(*a):
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle)
-def cpu_baseline(budget_s=10.0):
+def cpu_baseline(budget_s=12.0):
     """The host path, timed on this box's cores: AVX2 a += b over the same 1 GiB (the N=1
     workload), plus the reference's C1 config (2-rank 127.0.0.1 TCP ring, 4 MiB)."""
     import numpy as np
@@ -56,7 +56,7 @@ def cpu_baseline(budget_s=10.0):
     b = np.full(COUNT, 2.0, np.float32)
     t_start = time.time()
     t_mt = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, threads, 1)  # first touch / warm
-    iters = max(1, min(400, int((budget_s * 0.6) / max(t_mt, 1e-3))))
+    iters = max(1, min(2000, int((budget_s * 0.8) / max(t_mt, 1e-3))))
     t_mt = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, threads, iters)
     t_st = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, 1, 1)
     ok = L.oracle_verify_avx2(a.ctypes.data, COUNT, float(1.0 + 2.0 * (2 + iters))) == -1
