@@ -88,6 +88,7 @@ void Comm::setup_device_resources() {
   memset(h_ctl_, 0, 4096);
   hip_check(hipHostGetDevicePointer((void**)&d_ctl_, h_ctl_, 0), "ctl device pointer");
   hip_check(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "event");
+  hip_check(hipEventCreateWithFlags(&order_ev_, hipEventDisableTiming), "event");
   hip_check(hipDeviceSynchronize(), "init sync");
 }
 
@@ -254,6 +255,9 @@ void Comm::release() {
   stage_ = nullptr;
   stage_bytes_ = 0;
   if (done_) hipEventDestroy(done_);
+  if (order_ev_) hipEventDestroy(order_ev_);
+  order_ev_ = nullptr;
+  have_last_ = false;
   scratch_ = nullptr;
   mbox_ = nullptr;
   pair_seq_ = nullptr;
@@ -408,6 +412,14 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     warned_capture_ = true;
   }
 
+  // One communicator, one sequence of calls: the persistent kernels read and advance the
+  // per-pipeline FIFO counters, and the staging buffer is shared, so a call on another stream
+  // waits for the previous call (NCCL's rule: calls on a communicator are ordered).  Graph
+  // capture keeps its own order (the captured stream) and is left alone.
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (!capturing && have_last_ && stream != last_stream_)
+    hip_check(hipStreamWaitEvent(stream, order_ev_, 0), "order after previous call");
+
   const int n = nranks_;
   const size_t chunk = n > 0 ? count / (size_t)n : 0;  // mini_nccl.cu:69
   const size_t chunk_bytes = chunk * (size_t)esz;
@@ -446,6 +458,11 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
                 "tail copy");
     launch_ring_or_direct(ksend, krecv, chunk_bytes, dtype, op, stream);
     if (rr == Reach::kStaged) hip_check(hipMemcpyAsync(recv, stage_, bytes, hipMemcpyDefault, stream), "stage out");
+  }
+  if (!capturing) {
+    hip_check(hipEventRecord(order_ev_, stream), "order event");
+    last_stream_ = stream;
+    have_last_ = true;
   }
   if (cur_dev != device_) hipSetDevice(cur_dev);
   if (cfg_.blocking && cap == hipStreamCaptureStatusNone) return wait_for(stream);

@@ -78,6 +78,9 @@ class Comm {
   size_t stage_bytes_ = 0;
 
   hipEvent_t done_ = nullptr;
+  hipEvent_t order_ev_ = nullptr;     // recorded after every call (cross-stream ordering)
+  hipStream_t last_stream_ = nullptr;
+  bool have_last_ = false;
   ncclResult_t sticky_ = ncclSuccess;
   bool warned_capture_ = false;
 };

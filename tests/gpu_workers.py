@@ -169,6 +169,46 @@ def graph_rank(rank, n, port, env, replays, out_q):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def streams_rank(rank, n, port, env, calls, out_q):
+    """Stream-ordered calls (MINI_NCCL_BLOCKING=0) that alternate between two streams with no
+    host sync in between: the communicator orders call k+1 after call k whatever stream
+    each is on (NCCL's rule; two persistent kernels of one communicator must never overlap)."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        hip_rt.set_device(0)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        sts = [hip_rt.Stream(), hip_rt.Stream()]
+        count = (1 << 20) + 3
+        bufs, exps, rcs = [], [], []
+        for c in range(calls):
+            xs = O.random_inputs(n, count, "f32", seed=700 + c)
+            exps.append(O.allreduce(xs, "f32", "sum")[rank])
+            s, r = hip_rt.DeviceBuffer(count * 4), hip_rt.DeviceBuffer(count * 4)
+            s.upload(xs[rank])
+            bufs.append((s, r))
+        hip_rt.sync()
+        for c in range(calls):
+            s, r = bufs[c]
+            rcs.append(comm.all_reduce(s.ptr, r.ptr, count, M.ncclFloat, M.ncclSum, sts[c % 2].handle))
+        for st in sts:
+            st.sync()
+        bad = []
+        for c in range(calls):
+            got = bufs[c][1].download(np.float32, count)
+            bad.append(int((got.view(np.uint32) != exps[c].view(np.uint32)).sum()))
+            bufs[c][0].free()
+            bufs[c][1].free()
+        for st in sts:
+            st.destroy()
+        out_q.put((rank, {"rcs": rcs, "bad": bad, "async": comm.async_error(), "destroy": comm.destroy()}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
 def probe_rank(rank, n, port, env, out_q):
     """mncclCommLinkProbe is collective; afterwards an all-reduce must still be correct
     (the probe overwrote scratch slots while no message was in flight)."""

@@ -243,6 +243,18 @@ def test_allreduce_hip_graph_capture_and_replay(dev, algo):
         assert out[r]["eager_rc"] == 0 and out[r]["eager_bad"] == 0
 
 
+@pytest.mark.parametrize("algo", ["ring", "direct"])
+def test_calls_on_alternating_streams_are_ordered(dev, algo):
+    port = GW.free_port()
+    env = {"MINI_NCCL_TIMEOUT_MS": "20000", "MINI_NCCL_ALGO": algo, "MINI_NCCL_BLOCKING": "0", "MINI_NCCL_TUNE": "0"}
+    out = GW.run_ranks(GW.streams_rank, 3, lambda r: (r, 3, port, env, 6), 180)
+    assert sorted(out) == [0, 1, 2], out
+    for r in range(3):
+        assert "error" not in out[r], out[r]["error"]
+        assert out[r]["rcs"] == [0] * 6 and out[r]["bad"] == [0] * 6
+        assert out[r]["async"] == 0 and out[r]["destroy"] == 0
+
+
 def test_link_probe_then_allreduce(dev):
     port = GW.free_port()
     out = GW.run_ranks(GW.probe_rank, 3, lambda r: (r, 3, port, {"MINI_NCCL_TIMEOUT_MS": "20000"}), 180)
