@@ -313,6 +313,68 @@ def host_buffer_rate(M, torch, dist, comm, stream, n, max_over_ranks, mib=256, w
             "algbw_GBps": round(k * 4 / dt / 1e9, 2), "ms": round(dt * 1e3, 3), "ok": ok}
 
 
+def host_inclusive_n1(M, torch, dev, count, tdt, ndt, reps=3, piece_mib=64):
+    """N = 1, the path as the reference's callers use it (host memory in and out,
+    perf_test.cpp:78-79): a <- a + b with a and b in pinned host memory, copied H2D, reduced
+    by the same local_reduce kernel, the result copied D2H.  "serial": one copy in, one
+    launch, one copy out per step; "pipelined": the same in `piece_mib` pieces on a copy-in,
+    a compute and a copy-out stream (H2D of piece i+1 and D2H of piece i-1 overlap the
+    reduce of piece i).  Never the headline value."""
+    esz = torch.empty(0, dtype=tdt).element_size()
+    ha = torch.rand(count, dtype=torch.float32).to(tdt).pin_memory()
+    hb = torch.rand(count, dtype=torch.float32).to(tdt).pin_memory()
+    ref = (ha[: 1 << 20].float() + hb[: 1 << 20].float()).to(tdt)  # one correctly rounded add
+    a0 = ha[: 1 << 20].clone()
+    da = torch.empty(count, device=dev, dtype=tdt)
+    db = torch.empty(count, device=dev, dtype=tdt)
+    s_in, s_k, s_out = (torch.cuda.Stream(device=dev) for _ in range(3))
+    piece = (piece_mib << 20) // esz
+
+    def reduce_on(s, lo, hi):
+        rc = M.local_reduce(da[lo:].data_ptr(), da[lo:].data_ptr(), db[lo:].data_ptr(), hi - lo, ndt, M.ncclSum,
+                            s.cuda_stream)
+        if rc != 0:
+            raise M.NcclError(rc, "mncclLocalReduce")
+
+    def serial():
+        with torch.cuda.stream(s_k):
+            da.copy_(ha, non_blocking=True)
+            db.copy_(hb, non_blocking=True)
+            reduce_on(s_k, 0, count)
+            ha.copy_(da, non_blocking=True)
+        s_k.synchronize()
+
+    def pipelined():
+        for lo in range(0, count, piece):
+            hi = min(count, lo + piece)
+            e_in, e_k = torch.cuda.Event(), torch.cuda.Event()
+            with torch.cuda.stream(s_in):
+                da[lo:hi].copy_(ha[lo:hi], non_blocking=True)
+                db[lo:hi].copy_(hb[lo:hi], non_blocking=True)
+                e_in.record(s_in)
+            s_k.wait_event(e_in)
+            reduce_on(s_k, lo, hi)
+            e_k.record(s_k)
+            s_out.wait_event(e_k)
+            with torch.cuda.stream(s_out):
+                ha[lo:hi].copy_(da[lo:hi], non_blocking=True)
+        s_out.synchronize()
+
+    out = {"buffers": f"a, b: {count * esz >> 20} MiB {str(tdt).replace('torch.', '')} each in pinned host memory; "
+                      "result back in a (host)", "piece_MiB": piece_mib}
+    for name, fn in (("serial", serial), ("pipelined", pipelined)):
+        ha[: 1 << 20].copy_(a0)
+        fn()  # warm-up (also the correctness step: a was restored first)
+        ok = bool(torch.equal(ha[: 1 << 20], ref))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        dt = (time.perf_counter() - t0) / reps
+        out[name] = {"GBps": round(count * esz / dt / 1e9, 3), "ms": round(dt * 1e3, 3), "first_step_exact": ok}
+    del da, db
+    return out
+
+
 # ------------------------------------------------------------------ helpers
 def reduce_max(dist, x):
     """max over ranks of a host scalar through the harness's (gloo) process group"""
@@ -392,7 +454,7 @@ def main():
                     help="f32 = the headline; bf16/f16 = BASELINE.json configs[4] (C5)")
     ap.add_argument("--algo", choices=["auto", "ring", "direct"], default=os.environ.get("MINI_NCCL_ALGO", "auto"),
                     help="auto = the library default (ring at 2 ranks, direct from 3: same bits, every link)")
-    ap.add_argument("--no-alt", action="store_true", help="N>1: skip the second schedule and the RCCL reference")
+    ap.add_argument("--no-alt", action="store_true", help="skip the extras: N>1 the second schedule and the RCCL reference, N=1 the host-inclusive rate")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true", help="N>1: skip the configuration sweeps")
     ap.add_argument("--same-device", action="store_true",
@@ -633,6 +695,13 @@ def main():
             result["roofline"]["sum_kernel"] = {"error": sk_err or "failed on another rank"}
     # the extras below (RCCL's number, the sweeps) must never cost the headline line: if they
     # have not finished in EXTRAS_LIMIT_S, every rank gives up and rank 0 prints what it has
+    if n == 1 and not args.no_alt:
+        # PCIe-inclusive end-to-end rate (host buffers in and out); never `value`
+        arm(result)
+        try:
+            result["host_inclusive"] = host_inclusive_n1(M, torch, dev, count, tdt, ndt)
+        except Exception as e:
+            result["host_inclusive"] = {"error": str(e)[:200]}
     result["cpu_baseline"] = cpu
     if cpu_ring is not None:
         result["cpu_ring_baseline"] = cpu_ring
