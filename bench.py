@@ -386,6 +386,33 @@ def reduce_max(dist, x):
     return float(t.item())
 
 
+def peer_topology(dev, n, same_device):
+    """How this rank's GPU reaches every other rank's (device = rank on the node): the HIP
+    runtime's link type and hop count (hipExtGetLinkTypeAndHopCount; 4 = xGMI, 2 = PCIe) and
+    whether peer access is possible.  Diagnostics for tuning, never part of `value`."""
+    import ctypes
+    try:  # the HIP runtime torch (and libmini_nccl.so) already use, never a second copy
+        hip = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_LAZY)
+    except OSError:
+        return {"error": "HIP runtime not loaded"}
+    names = {0: "hypertransport", 1: "qpi", 2: "pcie", 3: "infiniband", 4: "xgmi"}
+    ndev = ctypes.c_int(0)
+    hip.hipGetDeviceCount(ctypes.byref(ndev))
+    out = {"visible_devices": ndev.value, "peers": []}
+    if same_device:
+        out["note"] = "every rank on one GPU (rehearsal)"
+        return out
+    for q in range(n):
+        if q == dev or q >= ndev.value:
+            continue
+        lt, hc, can = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_int(0)
+        rc = hip.hipExtGetLinkTypeAndHopCount(dev, q, ctypes.byref(lt), ctypes.byref(hc))
+        hip.hipDeviceCanAccessPeer(ctypes.byref(can), dev, q)
+        out["peers"].append({"device": q, "link": names.get(lt.value, lt.value) if rc == 0 else f"rc {rc}",
+                             "hops": hc.value if rc == 0 else None, "peer_access": bool(can.value)})
+    return out
+
+
 def pmc_traffic(key):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/pmc_summary.json)."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -601,10 +628,29 @@ def main():
         try:
             torch.cuda.synchronize()
             dist.barrier()
-            link["probe_next_GBps"] = round(max_over_ranks(-comm.link_probe(False, 0, 10)) * -1, 2)
-            link["probe_mesh_GBps_per_link"] = round(max_over_ranks(-comm.link_probe(True, 0, 10)) * -1, 2)
+            # min over ranks (the ceiling is set by the slowest link); max alongside for the spread
+            pn = comm.link_probe(False, 0, 10)
+            pm = comm.link_probe(True, 0, 10)
+            link["probe_next_GBps"] = round(max_over_ranks(-pn) * -1, 2)
+            link["probe_mesh_GBps_per_link"] = round(max_over_ranks(-pm) * -1, 2)
+            link["probe_next_max_GBps"] = round(max_over_ranks(pn), 2)
+            link["probe_mesh_max_GBps_per_link"] = round(max_over_ranks(pm), 2)
+            # other access forms over the same links (min over ranks), for the choice of form
+            # only: push non-temporal / default policy, pull (loads over the link)
+            var = {}
+            for name, form, pull in (("push_nt", "nt", False), ("push_plain", "plain", False),
+                                     ("pull_sys", "sys", True), ("pull_plain", "plain", True)):
+                for where, allp in (("next", False), ("mesh", True)):
+                    g = comm.link_probe(allp, 0, 10, form=form, pull=pull)
+                    var[f"{where}_{name}"] = round(max_over_ranks(-g) * -1, 2)
+            link["probe_variants_GBps_per_link"] = var
         except Exception as e:
             link["error"] = str(e)[:200]
+        if rank == 0:
+            try:
+                link["topology_rank0"] = peer_topology(local_rank, n, args.same_device)
+            except Exception as e:
+                link["topology_rank0"] = {"error": str(e)[:120]}
         wall, ev_ms, ok = run_algo(args.algo)
         ms = wall / args.steps * 1e3
         algbw = nbytes / (ms / 1e3) / 1e9

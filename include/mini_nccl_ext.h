@@ -61,10 +61,13 @@ ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info);
 ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo);
 
 /* Collective diagnostic: every rank streams `bytes` (0 = its whole scratch region) into the
- * next rank's scratch (allPeers = 0: one xGMI link per rank, the ring's) or into every peer's
- * at once (allPeers = 1: the mesh, the direct schedule's), `iters` times, with the hot path's
- * store form; *gbps = bytes per second per destination link.  Call only when no all-reduce is
- * in flight on any rank (it overwrites scratch slots). */
+ * next rank's scratch (allPeers bit 0 = 0: one xGMI link per rank, the ring's) or into every
+ * peer's at once (bit 0 = 1: the mesh, the direct schedule's), `iters` times, with the hot
+ * path's store form; *gbps = bytes per second per destination link.  Further bits of allPeers
+ * select variants for comparison: bits 1-2 = the remote accesses' cache policy (0 = the hot
+ * path's sc0 sc1, 1 = non-temporal, 2 = default), bit 3 = pull (load from the peers' scratch
+ * over the link instead of storing into it).  Call only when no all-reduce is in flight on any
+ * rank (it overwrites scratch slots). */
 ncclResult_t mncclCommLinkProbe(ncclComm_t comm, int allPeers, size_t bytes, int iters, double* gbps);
 
 /* library version, 10000*major + 100*minor + patch */

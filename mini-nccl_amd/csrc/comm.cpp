@@ -471,6 +471,11 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
 
 ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gbps) {
   if (nranks_ < 2 || iters < 1) return ncclInvalidArgument;
+  // mode bits (mini_nccl_ext.h): 0 every peer, 1-2 access form, 3 pull instead of push
+  const int form = (all_peers >> 1) & 3;
+  const bool pull = (all_peers >> 3) & 1;
+  if (form > kProbePlain || (all_peers & ~15)) return ncclInvalidArgument;
+  all_peers &= 1;
   const size_t region = scratch_region_bytes(wave_channels(), cfg_.slots, wave_slice());
   if (bytes == 0 || bytes > region) bytes = region;  // the probe writes this rank's region at each peer
   hip_check(hipSetDevice(device_), "hipSetDevice");
@@ -490,9 +495,10 @@ ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gb
   hip_check(hipEventCreate(&e1), "event");
   hip_check(hipDeviceSynchronize(), "probe sync");
   boot_.barrier();  // every rank idle and launching together
-  hip_check(launch_link_probe(src, dst.data(), (int)dst.size(), bytes, st), "probe warm-up");
+  hip_check(launch_link_probe(src, dst.data(), (int)dst.size(), bytes, form, pull, st), "probe warm-up");
   hip_check(hipEventRecord(e0, st), "event");
-  for (int i = 0; i < iters; ++i) hip_check(launch_link_probe(src, dst.data(), (int)dst.size(), bytes, st), "probe");
+  for (int i = 0; i < iters; ++i)
+    hip_check(launch_link_probe(src, dst.data(), (int)dst.size(), bytes, form, pull, st), "probe");
   hip_check(hipEventRecord(e1, st), "event");
   hip_check(hipEventSynchronize(e1), "probe wait");
   float ms = 0;

@@ -44,10 +44,14 @@ hipError_t launch_direct(int dtype, int op, bool vec, int channels, int threads,
 hipError_t launch_local_reduce(int dtype, int op, void* out, const void* local,
                                const void* incoming, uint64_t count, hipStream_t stream);
 
-// Link probe: every block streams `bytes` from `src` into each destination in `dst[0..ndst)`
-// with the hot path's store form (16-byte system-coherent buffer stores); blocks are spread
-// over destinations.  Used to measure the xGMI bandwidth the schedules are bound by.
-hipError_t launch_link_probe(const char* src, char* const* dst, int ndst, uint64_t bytes, hipStream_t stream);
+// Link probe: blocks spread over the `nremote` peers move `bytes` between `local` and each
+// remote[d]: pushes (pull = false, the schedules' direction) or loads over the link (pull =
+// true), with the remote side's cache policy `form`: kProbeSys = the hot path's 16-byte
+// sc0 sc1 accesses, kProbeNt = non-temporal, kProbePlain = default policy.  Used to measure
+// the xGMI bandwidth the schedules are bound by, and what other access forms would get.
+enum : int { kProbeSys = 0, kProbeNt = 1, kProbePlain = 2 };
+hipError_t launch_link_probe(char* local, char* const* remote, int nremote, uint64_t bytes, int form, bool pull,
+                             hipStream_t stream);
 
 bool dtype_supported(int dtype);
 int dtype_size(int dtype);

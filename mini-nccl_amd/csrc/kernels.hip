@@ -642,43 +642,71 @@ __global__ void __launch_bounds__(256) local_reduce_scalar(T* __restrict__ out, 
 
 // ---------------------------------------------------------------- link probe
 struct ProbeArgs {
-  const char* src;
-  char* dst[kMaxRanks];
-  int ndst;
+  char* local;
+  char* remote[kMaxRanks];
+  int nremote;
   uint64_t bytes;
 };
 
-// blocks [d * per, (d+1) * per) write destination d; 8 x 16 B per lane in flight
+// cache-policy bits of the probe's remote accesses (kProbe* in kernels.h): the hot path's
+// sc0 sc1, non-temporal, or the default policy
+template <int FORM> struct ProbeAux;
+template <> struct ProbeAux<kProbeSys> { static constexpr int v = kAuxSys; };
+template <> struct ProbeAux<kProbeNt> { static constexpr int v = 2; };
+template <> struct ProbeAux<kProbePlain> { static constexpr int v = 0; };
+
+// blocks [d * per, (d+1) * per) move `bytes` between `local` and remote d; 8 x 16 B per lane in
+// flight.  PULL = false: local -> remote (the schedules' pushes); true: remote -> local (loads
+// over the link, for comparison).
+template <int FORM, bool PULL>
 __global__ void __launch_bounds__(256) link_probe_kernel(ProbeArgs a) {
-  const int per = gridDim.x / a.ndst;
+  constexpr int AUX = ProbeAux<FORM>::v;
+  const int per = gridDim.x / a.nremote;
   const int d = blockIdx.x / per, b = blockIdx.x % per;
-  if (d >= a.ndst) return;
+  if (d >= a.nremote) return;
   const uint64_t nvec = a.bytes / 16;
-  const rsrc_t out = make_rsrc(a.dst[d], (uint32_t)a.bytes);
+  const rsrc_t rem = make_rsrc(a.remote[d], (uint32_t)a.bytes);
+  const rsrc_t loc = make_rsrc(a.local, (uint32_t)a.bytes);
   for (uint64_t base = (uint64_t)b * 256 * 8 + threadIdx.x; base < nvec; base += (uint64_t)per * 256 * 8) {
     v4u v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const uint64_t i = base + (uint64_t)u * 256;
-      if (i < nvec) v[u] = ld_g16(a.src + i * 16);
+      if (i < nvec)
+        v[u] = PULL ? __builtin_amdgcn_raw_buffer_load_b128(rem, (uint32_t)(i * 16), 0, AUX)
+                    : __builtin_amdgcn_raw_buffer_load_b128(loc, (uint32_t)(i * 16), 0, 2);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const uint64_t i = base + (uint64_t)u * 256;
-      if (i < nvec) st_slot16(out, (uint32_t)(i * 16), v[u]);
+      if (i < nvec) {
+        if (PULL) __builtin_amdgcn_raw_buffer_store_b128(v[u], loc, (uint32_t)(i * 16), 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b128(v[u], rem, (uint32_t)(i * 16), 0, AUX);
+      }
     }
   }
 }
 
-hipError_t launch_link_probe(const char* src, char* const* dst, int ndst, uint64_t bytes, hipStream_t st) {
-  if (ndst < 1 || ndst > kMaxRanks || bytes == 0 || bytes > 0xffffffffull) return hipErrorInvalidValue;
+hipError_t launch_link_probe(char* local, char* const* remote, int nremote, uint64_t bytes, int form, bool pull,
+                             hipStream_t st) {
+  if (nremote < 1 || nremote > kMaxRanks || bytes == 0 || bytes > 0xffffffffull) return hipErrorInvalidValue;
   ProbeArgs a;
-  a.src = src;
-  for (int i = 0; i < kMaxRanks; ++i) a.dst[i] = i < ndst ? dst[i] : nullptr;
-  a.ndst = ndst;
+  a.local = local;
+  for (int i = 0; i < kMaxRanks; ++i) a.remote[i] = i < nremote ? remote[i] : nullptr;
+  a.nremote = nremote;
   a.bytes = bytes;
-  const int per = 256 / ndst > 0 ? 256 / ndst : 1;
-  hipLaunchKernelGGL(link_probe_kernel, dim3(per * ndst), dim3(256), 0, st, a);
+  const int per = 256 / nremote > 0 ? 256 / nremote : 1;
+  const dim3 g(per * nremote), blk(256);
+#define PROBE_CASE(F)                                                        \
+  case F:                                                                    \
+    if (pull) hipLaunchKernelGGL((link_probe_kernel<F, true>), g, blk, 0, st, a); \
+    else hipLaunchKernelGGL((link_probe_kernel<F, false>), g, blk, 0, st, a);     \
+    break;
+  switch (form) {
+    PROBE_CASE(kProbeSys) PROBE_CASE(kProbeNt) PROBE_CASE(kProbePlain)
+    default: return hipErrorInvalidValue;
+  }
+#undef PROBE_CASE
   return hipGetLastError();
 }
 

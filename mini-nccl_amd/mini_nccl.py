@@ -133,11 +133,15 @@ class Comm:
         d["tune_ms"] = list(d["tune_ms"])
         return d
 
-    def link_probe(self, all_peers=False, nbytes=0, iters=10):
-        """GB/s per destination link (collective: every rank must call it)."""
+    PROBE_FORMS = {"sys": 0, "nt": 1, "plain": 2}
+
+    def link_probe(self, all_peers=False, nbytes=0, iters=10, form="sys", pull=False):
+        """GB/s per destination link (collective: every rank must call it).  form: the remote
+        accesses' cache policy ("sys" = the hot path's sc0 sc1, "nt", "plain"); pull: load
+        from the peers over the link instead of storing into them."""
         g = ctypes.c_double()
-        check(load().mncclCommLinkProbe(self.handle, int(bool(all_peers)), nbytes, iters, ctypes.byref(g)),
-              "mncclCommLinkProbe")
+        mode = int(bool(all_peers)) | (self.PROBE_FORMS[form] << 1) | (8 if pull else 0)
+        check(load().mncclCommLinkProbe(self.handle, mode, nbytes, iters, ctypes.byref(g)), "mncclCommLinkProbe")
         return g.value
 
     def set_algo(self, algo):
