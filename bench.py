@@ -231,6 +231,9 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
                 r = sweep_point(M, torch, dist, dev, n, rank, env, "ring", C4_COUNT, 3, max_over_ranks)
                 c4.append({"window": w, "slice": sl, **r})
         out["c4_ring_4GiB"] = c4
+        # the same 4 GiB with the library defaults (the direct schedule from 3 ranks)
+        r = sweep_point(M, torch, dist, dev, n, rank, {}, "direct", C4_COUNT, 3, max_over_ranks)
+        out["c4_direct_4GiB_defaults"] = r
     return out
 
 
