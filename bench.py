@@ -519,6 +519,10 @@ def main():
     M.load()
     if args.same_device:
         local_rank = 0
+    ndev = torch.cuda.device_count()
+    if 0 < ndev <= local_rank:  # a launcher that shows each rank only its own GPU(s)
+        log(f"LOCAL_RANK {local_rank} but {ndev} visible device(s): using device {local_rank % ndev}")
+        local_rank %= ndev
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist = None
