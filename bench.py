@@ -219,7 +219,9 @@ def verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stre
 
 def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
     out = {"buffer": "256 MiB fp32", "points": []}
-    for algo, env in SWEEP_POINTS:
+    for i, (algo, env) in enumerate(SWEEP_POINTS):
+        if rank == 0:
+            log(f"sweep {i + 1}/{len(SWEEP_POINTS)}: {algo} {env}")
         r = sweep_point(M, torch, dist, dev, n, rank, env, algo, 64 << 20, 5, max_over_ranks)
         out["points"].append({"algo": algo, "env": {k[len("MINI_NCCL_"):].lower(): v for k, v in env.items()}, **r})
     if with_c4:  # BASELINE.json configs[3]: ring, 4 GiB fp32, SLICE x WINDOW
@@ -228,6 +230,8 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
         for w in C4_WINDOWS:
             for sl in C4_SLICES:
                 env = {"MINI_NCCL_WINDOW_SIZE": w, "MINI_NCCL_SLICE_SIZE": sl}
+                if rank == 0:
+                    log(f"C4: ring {env}")
                 r = sweep_point(M, torch, dist, dev, n, rank, env, "ring", C4_COUNT, 3, max_over_ranks)
                 c4.append({"window": w, "slice": sl, **r})
         out["c4_ring_4GiB"] = c4
@@ -775,7 +779,11 @@ def main():
     if n > 1 and not args.no_alt:
         # the comparison ceiling: RCCL's all-reduce on the same buffer (torch.distributed nccl)
         pg = None
+        if rank == 0:
+            log("extras: RCCL reference")
         try:
+            if args.same_device:
+                raise RuntimeError("skipped: every rank on one GPU (RCCL needs one GPU per rank)")
             import torch.distributed as dist_
             pg = dist_.new_group(backend="nccl")
             x = torch.ones(count, device=dev, dtype=tdt)
@@ -799,6 +807,8 @@ def main():
             arm(result)
         # the reference's perf_test sizes (perf_test.cpp:69: 1/16/64/128 MiB), this library's
         # default schedule next to RCCL's all-reduce, device-resident fp32
+        if rank == 0:
+            log("extras: sizes")
         try:
             if args.dtype == "f32":
                 result["sizes"] = size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks)
@@ -809,6 +819,8 @@ def main():
         # the reference's own usage: host buffers in, host buffers out (perf_test.cpp:78-79);
         # pinned memory is mapped into the kernel, so this is the PCIe-inclusive end-to-end rate
         if args.dtype == "f32":
+            if rank == 0:
+                log("extras: host buffers")
             result["host_buffers"] = host_buffer_rate(M, torch, dist, comm, stream, n, max_over_ranks)
             if rank == 0:
                 arm(result)

@@ -42,3 +42,13 @@ def test_banners_on_fd1_go_to_stderr():
     assert r.returncode == 0
     assert r.stdout.strip() == json.dumps({"value": 4.0})
     assert "native banner" in r.stderr
+
+
+def test_sigterm_after_arm_prints_the_armed_line():
+    # a launcher's time limit during the extras still leaves the headline on stdout
+    r = _run("bench.arm({'value': 5.0})\n"
+             "os.kill(os.getpid(), 15)\n"
+             "import time; time.sleep(5)\n")
+    assert r.returncode == -15
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert [json.loads(x) for x in lines] == [{"value": 5.0}]

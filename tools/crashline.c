@@ -1,7 +1,8 @@
 /* crashline.c -- bench.py insurance: if a process dies on a fatal signal (a GPU fault makes the
  * HSA runtime call abort(); a bad pointer gives SIGSEGV / SIGBUS) after the headline was
- * measured, write the last armed JSON line to the given fd before dying, so the one-line
- * contract still holds.  Only async-signal-safe calls (write, signal, raise) in the handler.
+ * measured, or is terminated (SIGTERM: a launcher's time limit, torchrun passing one on), write
+ * the last armed JSON line to the given fd before dying, so the one-line contract still holds.
+ * Only async-signal-safe calls (write, signal, raise) in the handler.
  *
  *   crashline_arm(fd, line)  copy `line` (+ '\n') into a static buffer; install the handlers
  *   crashline_disarm()       forget the line (the normal emit path printed it)
@@ -49,6 +50,7 @@ int crashline_arm(int fd, const char* line) {
     sigaction(SIGBUS, &sa, NULL);
     sigaction(SIGFPE, &sa, NULL);
     sigaction(SIGILL, &sa, NULL);
+    sigaction(SIGTERM, &sa, NULL);
   }
   return 0;
 }
