@@ -132,7 +132,7 @@ def cpu_ring_baseline(n, budget_s=4.0):
 # own communicator (the knobs are read at ncclCommInitRank, as the reference's Config).
 SWEEP_POINTS = [
     # (algo, knobs over the library defaults: 256 one-wave workgroups, 128 KiB slices, 2 slots,
-    #  no hand-off fences, overlapped direct phases)
+    #  no hand-off fences, overlapped direct phases, push)
     ("direct", {}), ("direct", {"MINI_NCCL_CHANNELS": 64, "MINI_NCCL_THREADS": 256}),
     ("direct", {"MINI_NCCL_THREADS": 128}), ("direct", {"MINI_NCCL_CHANNELS": 512}),
     ("direct", {"MINI_NCCL_SLOTS": 4}), ("direct", {"MINI_NCCL_SLICE_SIZE": 524288}),
@@ -141,6 +141,8 @@ SWEEP_POINTS = [
     ("direct", {"MINI_NCCL_CHANNELS": 128}),
     ("ring", {}), ("ring", {"MINI_NCCL_THREADS": 128}), ("ring", {"MINI_NCCL_SLOTS": 4}),
     ("ring", {"MINI_NCCL_SLICE_SIZE": 524288}), ("ring", {"MINI_NCCL_SYS_FENCE": 1}),
+    # slots in the sender's scratch, loaded over the link (pull) instead of stored into (push)
+    ("direct", {"MINI_NCCL_PULL": 1}), ("ring", {"MINI_NCCL_PULL": 1}),
 ]
 C4_SLICES = [65536, 131072, 262144, 1048576]
 C4_WINDOWS = [16, 32, 64]

@@ -42,7 +42,7 @@ struct PeerInfo {
   uint64_t slice, scratch_bytes, mbox_bytes;
   int32_t channels, slots, threads, abi;
   uint64_t min_slice;
-  int32_t depth, overlap;
+  int32_t depth, overlap, pull, pad1;
   hipIpcMemHandle_t scratch_h, mbox_h;
   uint64_t scratch_ptr, mbox_ptr;  // raw addresses for ranks living in the same process
 };
@@ -115,6 +115,7 @@ void Comm::exchange_and_map() {
   me.min_slice = cfg_.min_slice;
   me.depth = cfg_.pipe_depth;
   me.overlap = cfg_.direct_overlap;
+  me.pull = cfg_.pull;
   hip_check(hipIpcGetMemHandle(&me.scratch_h, scratch_), "ipc handle scratch");
   hip_check(hipIpcGetMemHandle(&me.mbox_h, mbox_), "ipc handle mailbox");
   me.scratch_ptr = (uint64_t)(uintptr_t)scratch_;
@@ -128,10 +129,10 @@ void Comm::exchange_and_map() {
       throw std::runtime_error("bootstrap: inconsistent rank records");
     if (p.host != me.host) throw std::runtime_error("rank " + std::to_string(q) + " is on another host: only one node is supported");
     if (p.slice != me.slice || p.channels != me.channels || p.slots != me.slots || p.threads != me.threads ||
-        p.min_slice != me.min_slice || p.depth != me.depth || p.overlap != me.overlap)
+        p.min_slice != me.min_slice || p.depth != me.depth || p.overlap != me.overlap || p.pull != me.pull)
       throw std::invalid_argument(
           "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SLOTS / CHANNELS / THREADS / MIN_SLICE / PIPE_DEPTH / "
-          "DIRECT_OVERLAP differ between ranks");
+          "DIRECT_OVERLAP / PULL differ between ranks");
   }
   for (int q = 0; q < nranks_; ++q) {
     if (q == rank_) {
@@ -382,6 +383,7 @@ void Comm::launch_ring_or_direct(const void* send, void* recv, size_t chunk_byte
   p.timeout_ticks = (uint64_t)(cfg_.timeout_ms * 1e5);  // s_memrealtime runs at 100 MHz
   p.sys_fence = cfg_.sys_fence;
   p.direct_overlap = cfg_.direct_overlap;
+  p.pull = cfg_.pull;
   // 16-byte vector path whenever every message's local base is dword-aligned (vectors may
   // straddle 16-byte boundaries on the local side; each message's last len % 16 bytes go
   // element by element); element-wise path otherwise (2-byte types with odd chunks)

@@ -1,6 +1,8 @@
 // config.cpp -- see config.h.
 #include "config.h"
 
+#include "schedule.h"
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -48,7 +50,7 @@ Config Config::from_env() {
   if (c.channels > 1024) c.channels = 1024;
   c.threads = (int)env_int("MINI_NCCL_THREADS", 64);
   if (c.threads < 64) c.threads = 64;
-  if (c.threads > 1024) c.threads = 1024;
+  if (c.threads > kMaxThreads) c.threads = kMaxThreads;  // the kernels' launch bound (kernels.h)
   c.threads &= ~63;
   const char* a = std::getenv("MINI_NCCL_ALGO");
   if (a && *a) {
@@ -65,6 +67,7 @@ Config Config::from_env() {
   c.pipe_depth = (int)env_int("MINI_NCCL_PIPE_DEPTH", 1);
   if (c.pipe_depth < 1) c.pipe_depth = 1;
   c.direct_overlap = env_int("MINI_NCCL_DIRECT_OVERLAP", 1) != 0;
+  c.pull = env_int("MINI_NCCL_PULL", 0) != 0;
   c.tune = env_int("MINI_NCCL_TUNE", 1) != 0;
   long long tb = env_int("MINI_NCCL_TUNE_BYTES", 64LL << 20);
   if (tb < (1LL << 20)) tb = 1LL << 20;
@@ -82,10 +85,10 @@ std::string Config::describe() const {
   char b[320];
   snprintf(b, sizeof b,
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, algo=%s, blocking=%d, "
-           "sys_fence=%d, min_slice=%zu, depth=%d, tune=%d, stage_host=%d, timeout=%.0f ms, port=%d",
+           "sys_fence=%d, min_slice=%zu, depth=%d, pull=%d, tune=%d, stage_host=%d, timeout=%.0f ms, port=%d",
            slice_size, window_size, signal_batch, slots, channels, threads,
            algo < 0 ? "auto" : algo ? "direct" : "ring", blocking,
-           sys_fence, min_slice, pipe_depth, tune, stage_host, timeout_ms, port);
+           sys_fence, min_slice, pipe_depth, pull, tune, stage_host, timeout_ms, port);
   return b;
 }
 

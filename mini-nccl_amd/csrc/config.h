@@ -22,6 +22,7 @@ struct Config {
   size_t min_slice = 1024;         // MINI_NCCL_MIN_SLICE smallest adaptive payload (>= SLICE_SIZE: adaptation off)
   int pipe_depth = 1;              // MINI_NCCL_PIPE_DEPTH slices per pipeline targeted for small calls
   int direct_overlap = 1;          // MINI_NCCL_DIRECT_OVERLAP next iteration's raw pushes before this one's results
+  int pull = 0;                    // MINI_NCCL_PULL   1: slots in the sender's scratch, loaded over the link
   int tune = 1;                    // MINI_NCCL_TUNE   auto algo: time both schedules at init (n >= 3)
   size_t tune_bytes = 64u << 20;   // MINI_NCCL_TUNE_BYTES per-rank buffer of that calibration
   int stage_host = 0;              // MINI_NCCL_STAGE_HOST pinned host buffers: 0 = kernel maps them, 1 = staged copy

@@ -30,6 +30,7 @@ struct CollParams {
   uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
   int32_t sys_fence;       // system-scope release fence before each ready flag
   int32_t direct_overlap;  // direct: next iteration's raw pushes before this one's results
+  int32_t pull;            // slots in the sender's scratch, loaded over the link (schedule.h)
 };
 
 constexpr int kMaxRanks = 16;

@@ -31,6 +31,10 @@
 //    consistent); nothing is reset per call and stale flags cannot satisfy a wait.
 //  * every spin is bounded (MINI_NCCL_TIMEOUT_MS via s_memrealtime) and also exits on
 //    the host abort word or a peer's ABORT; the kernel always terminates.
+//  * MINI_NCCL_PULL=1 moves the slots to the sender's scratch (schedule.h slot_owner): the
+//    producer's sc0 sc1 stores stay local, the consumer's sc0 sc1 loads cross the link; the
+//    flags, credits and the drain-before-flag order are unchanged, and so is the argument
+//    above (uncached memory, system-scope accesses on both sides).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -140,6 +144,13 @@ template <> struct Scal<8> {
   }
 };
 
+// message `seq` from `src` to `dst` on pipeline w (schedule.h: push = receiver's scratch, pull =
+// sender's); peer_scratch[rank] is this rank's own scratch
+__device__ __forceinline__ char* msg_slot(const CollParams& p, int C, int src, int dst, int w, u64 seq) {
+  return p.peer_scratch[slot_owner(p.pull, src, dst)] +
+         scratch_slot_off(C, p.nslots, p.slot_bytes, slot_region(p.pull, src, dst), w, seq);
+}
+
 // ---------------------------------------------------------------- bounded waits
 struct Ctl {
   uint32_t* status;
@@ -160,9 +171,10 @@ __device__ __forceinline__ void record_timeout(const Ctl& c, const u64* flag, u6
   __hip_atomic_store(diag + 2, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// lane-0 spin until *flag >= target; false on timeout / abort (status already set)
-__device__ __noinline__ bool wait_ge(const u64* flag, u64 target, const Ctl& c) {
-  if (ld_sys(flag) >= target) return true;
+// lane-0 spin until *flag >= target; false on timeout / abort (status already set).  The
+// spin is out of line (kept out of the message bodies' code and registers); Ctl goes by value
+// so it travels in registers -- by reference it had to live in scratch memory.
+__device__ __noinline__ bool wait_ge_spin(const u64* flag, u64 target, const Ctl c) {
   const u64 t0 = __builtin_amdgcn_s_memrealtime();
   for (uint32_t polls = 1;; ++polls) {
     __builtin_amdgcn_s_sleep(1);
@@ -178,6 +190,12 @@ __device__ __noinline__ bool wait_ge(const u64* flag, u64 target, const Ctl& c) 
       }
     }
   }
+}
+
+// the common case (the flag is already there) costs one load and no call
+__device__ __forceinline__ bool wait_ge(const u64* flag, u64 target, const Ctl& c) {
+  if (ld_sys(flag) >= target) return true;
+  return wait_ge_spin(flag, target, c);
 }
 
 // After a READY poll.  Every load of handed-off bytes is an sc0 sc1 buffer load of uncached
@@ -315,7 +333,7 @@ __device__ __forceinline__ WaveId wave_id() {
 
 // ---------------------------------------------------------------- ring kernel
 template <typename T, int OPC, bool VEC>
-__global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
+__global__ void __launch_bounds__(kMaxThreads) ring_kernel(CollParams p) {
   const WaveId id = wave_id();
   const int lane = id.lane, w = id.w, C = id.C;
   const int n = p.n, r = p.rank, K = p.nslots;
@@ -350,8 +368,8 @@ __global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
       if (o.recv_msg >= 0) acquire_sys(p.sys_fence);
       if (len) {
         const u64 coff = (u64)o.chunk * p.chunk_bytes + soff;
-        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, prev, w, rseq), len);
-        const rsrc_t out = make_rsrc(p.peer_scratch[next] + scratch_slot_off(C, K, p.slot_bytes, r, w, sseq), len);
+        const rsrc_t in = make_rsrc(msg_slot(p, C, prev, r, w, rseq), len);
+        const rsrc_t out = make_rsrc(msg_slot(p, C, r, next, w, sseq), len);
         const char* lsrc = p.send + coff;
         char* ldst = p.recv + coff;
         switch (o.kind) {
@@ -380,21 +398,21 @@ __global__ void __launch_bounds__(1024) ring_kernel(CollParams p) {
 template <typename T, int OPC>
 __device__ __forceinline__ void fold_scalar(const CollParams& p, const char* lsrc, char* ldst, const u64* rx0,
                                             const u64* tx1, uint32_t nbytes, int w, int C, int lane, uint32_t off0) {
-  const int n = p.n, r = p.rank, K = p.nslots;
+  const int n = p.n, r = p.rank;
   typedef typename Scal<sizeof(T)>::U Us;
   const uint32_t ne = nbytes / sizeof(T);
   for (uint32_t i = off0 / sizeof(T) + lane; i < ne; i += 64) {
     T acc = reinterpret_cast<const T*>(lsrc)[i];
     for (int k = 1; k < n; ++k) {
       const int q = direct_peer(n, r, k);
-      const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q]), nbytes);
+      const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q]), nbytes);
       const T x = __builtin_bit_cast(T, Scal<sizeof(T)>::ld(in, i * (uint32_t)sizeof(T)));
       acc = Op<T, OPC>::f(x, acc);
     }
     reinterpret_cast<T*>(ldst)[i] = acc;
     for (int k = 1; k < n; ++k) {
       const int d = direct_peer(n, r, k);
-      const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, tx1[d]), nbytes);
+      const rsrc_t out = make_rsrc(msg_slot(p, C, r, d, w, tx1[d]), nbytes);
       Scal<sizeof(T)>::st(out, i * (uint32_t)sizeof(T), __builtin_bit_cast(Us, acc));
     }
   }
@@ -411,7 +429,7 @@ constexpr int kFoldU = MNCCL_FOLD_U;  // vectors per lane per batch in the fold 
 template <typename T, int OPC, bool VEC>
 __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* lsrc, char* ldst, const u64* rx0,
                                               const u64* tx1, uint32_t nbytes, int w, int C, int lane) {
-  const int n = p.n, r = p.rank, K = p.nslots;
+  const int n = p.n, r = p.rank;
   if (VEC) {
     constexpr int U = kFoldU;
     const uint32_t nvec = nbytes >> 4;
@@ -424,14 +442,14 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
       for (int u = 0; u < U; ++u) acc[u] = ld_g16(lsrc + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16);
       {
         const int q = direct_peer(n, r, 1);
-        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q]), nbytes);
+        const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q]), nbytes);
 #pragma unroll
         for (int u = 0; u < U; ++u) cur[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
       }
       for (int k = 1; k < n; ++k) {
         if (k + 1 < n) {
           const int q = direct_peer(n, r, k + 1);
-          const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q]), nbytes);
+          const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q]), nbytes);
 #pragma unroll
           for (int u = 0; u < U; ++u) nxt[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
         }
@@ -444,7 +462,7 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
       for (int u = 0; u < U; ++u) st_g16(ldst + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
       for (int k = 1; k < n; ++k) {
         const int d = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));  // staggered like phase A
-        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, tx1[d]), nbytes);
+        const rsrc_t out = make_rsrc(msg_slot(p, C, r, d, w, tx1[d]), nbytes);
 #pragma unroll
         for (int u = 0; u < U; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
       }
@@ -454,13 +472,13 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
       v4u acc = ld_g16(lsrc + (size_t)i * 16);
       for (int k = 1; k < n; ++k) {
         const int q = direct_peer(n, r, k);
-        const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q]), nbytes);
+        const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q]), nbytes);
         acc = reduce16<T, OPC>(ld_slot16(in, i * 16), acc);
       }
       st_g16(ldst + (size_t)i * 16, acc);
       for (int k = 1; k < n; ++k) {
         const int d = direct_peer(n, r, k);
-        const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, tx1[d]), nbytes);
+        const rsrc_t out = make_rsrc(msg_slot(p, C, r, d, w, tx1[d]), nbytes);
         st_slot16(out, i * 16, acc);
       }
     }
@@ -470,7 +488,7 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
   }
 }
 
-constexpr int kMaxWaves = 16;
+constexpr int kMaxWaves = kMaxThreads / 64;
 
 // Phase A's raw pushes are pure remote stores.  One vmcnt counts loads and stores in issue
 // order, so a batch's loads cannot be used before the previous batch's stores are acknowledged:
@@ -483,7 +501,7 @@ constexpr int kMaxWaves = 16;
 constexpr int kPushU = MNCCL_PUSH_U;
 
 template <typename T, int OPC, bool VEC>
-__global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
+__global__ void __launch_bounds__(kMaxThreads) direct_kernel(CollParams p) {
   const WaveId id = wave_id();
   const int lane = id.lane, w = id.w, C = id.C, wv = id.wv;
   const int n = p.n, r = p.rank, K = p.nslots;
@@ -528,7 +546,7 @@ __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
         if (seq0 + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, d, w), seq0 + 1 - K, ctl, lane))
           goto aborted;
         if (len) {
-          const rsrc_t out = make_rsrc(p.peer_scratch[d] + scratch_slot_off(C, K, p.slot_bytes, r, w, seq0), len);
+          const rsrc_t out = make_rsrc(msg_slot(p, C, r, d, w, seq0), len);
           const u64 coff = (u64)d * p.chunk_bytes + soff;
           move<T, OPC, VEC, kSend, kPushU>(p.send + coff, nullptr, out, out, len, lane);
         }
@@ -579,7 +597,7 @@ __global__ void __launch_bounds__(1024) direct_kernel(CollParams p) {
       if (len) {
         for (int k = 1; k < n; ++k) {
           const int q = direct_peer(n, r, k);
-          const rsrc_t in = make_rsrc(p.scratch + scratch_slot_off(C, K, p.slot_bytes, q, w, rx0[q] + 1), len);
+          const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q] + 1), len);
           const u64 coff = (u64)q * p.chunk_bytes + soff;
           move<T, OPC, VEC, kCopy>(nullptr, p.recv + coff, in, in, len, lane);
         }

@@ -47,6 +47,11 @@ struct RingOp {
   int recv_msg;  // message index received from r-1, or -1
 };
 
+// Threads per workgroup of the persistent kernels (MINI_NCCL_THREADS is clamped to it): the
+// launch bound lets the compiler give a pipeline's wave up to 512 VGPRs instead of the 128 a
+// 1024-thread bound allows (the direct fold spilled at 128); one wave per workgroup is the default.
+constexpr int kMaxThreads = 256;
+
 MNCCL_HD int mod_n(int a, int n) { return ((a % n) + n) % n; }
 
 MNCCL_HD int ring_num_ops(int n) { return 2 * n - 1; }
@@ -141,6 +146,13 @@ MNCCL_HD uint64_t scratch_slot_off(int C, int slots, uint64_t slice_bytes, int s
   return (uint64_t)src * scratch_region_bytes(C, slots, slice_bytes) +
          ((uint64_t)w * slots + (seq % (uint64_t)slots)) * slice_bytes;
 }
+
+// Where message `seq` from rank `src` to rank `dst` (pipeline w) lives.  Push (default): in the
+// receiver's scratch, region src -- the sender's stores cross the link.  Pull
+// (MINI_NCCL_PULL=1): in the sender's own scratch, region dst -- the receiver's loads cross the
+// link.  Flags, credits and sequence numbers are the same either way.
+MNCCL_HD int slot_owner(int pull, int src, int dst) { return pull ? src : dst; }
+MNCCL_HD int slot_region(int pull, int src, int dst) { return pull ? dst : src; }
 
 // Kernel status bits (host-mapped status word)
 enum : uint32_t { kStatusTimeout = 1u, kStatusHostAbort = 2u, kStatusRemoteAbort = 4u };

@@ -28,7 +28,7 @@ float apply(int op, float a, float b) {
 }
 
 struct World {
-  int n, C, K, op, algo, overlap = 1;
+  int n, C, K, op, algo, overlap = 1, pull = 0;
   uint64_t slice, slot_bytes, chunk_bytes, nslices;  // payload per message, slot stride
   uint32_t iters;
   std::vector<const float*> send;
@@ -37,8 +37,10 @@ struct World {
   std::vector<std::vector<uint64_t>> mbox;    // per rank
   std::vector<std::vector<uint64_t>> tx_seq, rx_seq;  // per rank: [peer * C + w]
 
-  char* slot(int owner, int src, int w, uint64_t seq) {
-    return scratch[owner].data() + scratch_slot_off(C, K, slot_bytes, src, w, seq);
+  // message `seq` from src to dst on pipeline w (schedule.h: push / pull placement)
+  char* slot(int src, int dst, int w, uint64_t seq) {
+    return scratch[slot_owner(pull, src, dst)].data() +
+           scratch_slot_off(C, K, slot_bytes, slot_region(pull, src, dst), w, seq);
   }
   uint64_t& ready(int owner, int src, int w) { return mbox[owner][mbox_ready(C, src, w)]; }
   uint64_t& credit(int owner, int dst, int w) { return mbox[owner][mbox_credit(n, C, dst, w)]; }
@@ -86,8 +88,8 @@ bool ring_step(World& W, Prog& P) {
     const uint64_t coff = (uint64_t)o.chunk * W.chunk_bytes + soff;
     const float* local = (const float*)((const char*)W.send[r] + coff);
     float* recv = (float*)((char*)W.recv[r] + coff);
-    const float* in = o.recv_msg >= 0 ? (const float*)W.slot(r, prev, w, rseq) : nullptr;
-    float* out = o.send_msg >= 0 ? (float*)W.slot(next, r, w, sseq) : nullptr;
+    const float* in = o.recv_msg >= 0 ? (const float*)W.slot(prev, r, w, rseq) : nullptr;
+    float* out = o.send_msg >= 0 ? (float*)W.slot(r, next, w, sseq) : nullptr;
     do_move(o.kind, W.op, local, in, recv, out, len);
   }
   if (o.send_msg >= 0) W.ready(next, r, w) = sseq + 1;
@@ -124,7 +126,7 @@ bool direct_step(World& W, Prog& P) {
       if (len) {
         const uint64_t coff = (uint64_t)d * W.chunk_bytes + soff;
         do_move(kSend, W.op, (const float*)((const char*)W.send[r] + coff), nullptr, nullptr,
-                (float*)W.slot(d, r, w, tx0(d)), len);
+                (float*)W.slot(r, d, w, tx0(d)), len);
       }
     }
     for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx0(direct_peer(n, r, k)) + 1;
@@ -142,12 +144,12 @@ bool direct_step(World& W, Prog& P) {
         float acc = local[i];
         for (int k = 1; k < n; ++k) {
           const int q = direct_peer(n, r, k);
-          acc = apply(W.op, ((const float*)W.slot(r, q, w, rx0(q)))[i], acc);
+          acc = apply(W.op, ((const float*)W.slot(q, r, w, rx0(q)))[i], acc);
         }
         recv[i] = acc;
         for (int k = 1; k < n; ++k) {
           const int d = direct_peer(n, r, k);
-          ((float*)W.slot(d, r, w, tx0(d) + 1))[i] = acc;
+          ((float*)W.slot(r, d, w, tx0(d) + 1))[i] = acc;
         }
       }
     }
@@ -160,7 +162,7 @@ bool direct_step(World& W, Prog& P) {
       const int q = direct_peer(n, r, k);
       if (len) {
         const uint64_t coff = (uint64_t)q * W.chunk_bytes + soff;
-        do_move(kCopy, W.op, nullptr, (const float*)W.slot(r, q, w, rx0(q) + 1), (float*)((char*)W.recv[r] + coff),
+        do_move(kCopy, W.op, nullptr, (const float*)W.slot(q, r, w, rx0(q) + 1), (float*)((char*)W.recv[r] + coff),
                 nullptr, len);
       }
     }
@@ -188,12 +190,13 @@ uint64_t mnccl_effective_slice(uint64_t chunk_bytes, int channels, uint64_t slic
 // (pseudo-random), exploring different interleavings.  Returns 0, -1 on deadlock,
 // -2 on bad arguments.  *steps_out = ops executed.
 int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, int n, uint64_t count, int op,
-                        uint64_t slice_bytes, uint64_t min_slice, int direct_overlap, int channels, int slots,
-                        int calls, uint64_t schedule_seed, uint64_t* steps_out) {
+                        uint64_t slice_bytes, uint64_t min_slice, int direct_overlap, int pull, int channels,
+                        int slots, int calls, uint64_t schedule_seed, uint64_t* steps_out) {
   if (n < 1 || n > 16 || channels < 1 || slots < 1 || slice_bytes < 4 || slice_bytes % 4) return -2;
   World W;
   W.n = n; W.C = channels; W.K = slots; W.op = op; W.algo = algo; W.slot_bytes = slice_bytes;
   W.overlap = direct_overlap;
+  W.pull = pull;
   const uint64_t chunk = count / (uint64_t)n;
   W.chunk_bytes = chunk * 4;
   // as Comm::launch_ring_or_direct: adaptive payload (min_slice 0 = off), fixed slot stride

@@ -13,8 +13,8 @@
 
 extern "C" {
 int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, int n, uint64_t count, int op,
-                        uint64_t slice_bytes, uint64_t min_slice, int direct_overlap, int channels, int slots,
-                        int calls, uint64_t schedule_seed, uint64_t* steps_out);
+                        uint64_t slice_bytes, uint64_t min_slice, int direct_overlap, int pull, int channels,
+                        int slots, int calls, uint64_t schedule_seed, uint64_t* steps_out);
 int mnccl_bootstrap_selftest(int rank, int nranks, const char* ip, int port, int timeout_ms);
 int mnccl_config_describe(char* buf, int len);
 }
@@ -34,8 +34,9 @@ static int sim_case(int algo, int n, uint64_t count, uint64_t slice, uint64_t mi
   }
   uint64_t steps = 0;
   const int mask = algo ? (1 << calls) - 1 : 0;
-  const int rc = mnccl_sim_allreduce(mask, sp.data(), rp.data(), n, count, 0, slice, min_slice, overlap, channels,
-                                     slots, calls, seed, &steps);
+  // pull placement on odd seeds: the same protocol with every slot in the sender's scratch
+  const int rc = mnccl_sim_allreduce(mask, sp.data(), rp.data(), n, count, 0, slice, min_slice, overlap, (int)(seed & 1),
+                                     channels, slots, calls, seed, &steps);
   if (rc != 0) return 1;
   // every rank holds the same bits in the body (the count % n tail keeps each rank's own
   // input; the oracle comparison lives in the Python tests)

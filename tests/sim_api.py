@@ -18,7 +18,7 @@ def load():
     if _lib is None:
         L = ctypes.CDLL(LIB)
         vp, u64, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
-        L.mnccl_sim_allreduce.argtypes = [i, ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64, u64, i, i, i, i, u64,
+        L.mnccl_sim_allreduce.argtypes = [i, ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64, u64, i, i, i, i, i, u64,
                                           ctypes.POINTER(u64)]
         L.mnccl_direct_phase_at.argtypes = [ctypes.c_uint32, ctypes.c_uint32, i, ctypes.POINTER(i),
                                             ctypes.POINTER(ctypes.c_uint32)]
@@ -30,7 +30,8 @@ def load():
     return _lib
 
 
-def allreduce(inputs, algo=0, op=0, slice_bytes=1024, channels=4, slots=2, calls=1, seed=0, algos=None, min_slice=0, direct_overlap=1):
+def allreduce(inputs, algo=0, op=0, slice_bytes=1024, channels=4, slots=2, calls=1, seed=0, algos=None, min_slice=0,
+              direct_overlap=1, pull=0):
     """fp32 all-reduce of `inputs` (one array per rank) through the simulated kernels,
     `calls` times on one communicator state (schedule `algo` for every call, or the
     per-call list `algos`).  Returns (outputs, steps); raises RuntimeError on deadlock."""
@@ -45,7 +46,8 @@ def allreduce(inputs, algo=0, op=0, slice_bytes=1024, channels=4, slots=2, calls
     sp = (ctypes.c_void_p * n)(*[s.ctypes.data for s in sends])
     rp = (ctypes.c_void_p * n)(*[r.ctypes.data for r in recvs])
     steps = ctypes.c_uint64()
-    rc = load().mnccl_sim_allreduce(mask, sp, rp, n, sends[0].size, op, slice_bytes, min_slice, direct_overlap, channels, slots,
+    rc = load().mnccl_sim_allreduce(mask, sp, rp, n, sends[0].size, op, slice_bytes, min_slice, direct_overlap, pull,
+                                    channels, slots,
                                     calls, seed,
                                     ctypes.byref(steps))
     if rc == -1:

@@ -273,13 +273,26 @@ def test_single_rank_is_copy_only(dev):
     _run_allreduce(1, cases)
 
 
-def test_mismatched_config_is_invalid_usage(dev):
+@pytest.mark.parametrize("knob,values", [("MINI_NCCL_SLICE_SIZE", ("131072", "65536")), ("MINI_NCCL_PULL", ("0", "1"))])
+def test_mismatched_config_is_invalid_usage(dev, knob, values):
     import mini_nccl as M
     port = GW.free_port()
-    env = {0: {"MINI_NCCL_SLICE_SIZE": "131072"}, 1: {"MINI_NCCL_SLICE_SIZE": "65536"}}
+    env = {0: {knob: values[0]}, 1: {knob: values[1]}}
     out = GW.run_ranks(GW.init_rank, 2, lambda r: (r, 2, port, env), 120)
     assert sorted(out) == [0, 1], out
     assert out[0]["rc"] == M.ncclInvalidUsage and out[1]["rc"] == M.ncclInvalidUsage
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("n", [2, 3])
+def test_pull_placement(dev, algo, n):
+    # MINI_NCCL_PULL=1: every slot in the sender's scratch, loaded by the receiver over the link
+    # (the comparison form for xGMI, csrc/schedule.h); same flags and credits, same bits
+    cases = [_case(count=(1 << 20) + 3, algo=algo, seed=31),
+             _case(dtype="bf16", op="max", count=77777, algo=algo, seed=32, special=True),
+             _case(dtype="f64", count=50001, algo=algo, inplace=True, calls=2, seed=33),
+             _case(dtype="i32", op="prod", count=4099, algo=algo, seed=34)]
+    _run_allreduce(n, cases, env={"MINI_NCCL_PULL": "1"})
 
 
 def test_count_beyond_int32(dev):

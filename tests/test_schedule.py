@@ -148,3 +148,17 @@ def test_direct_phase_order_is_a_permutation(sim_lib):
                 assert pos[(0, t)] < pos[(1, t)] < pos[(2, t)]
                 if overlap and t + 1 < iters:
                     assert pos[(0, t + 1)] < pos[(2, t)]
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("seed", range(1, 9))
+def test_sim_pull_placement(oracle_lib, sim_lib, algo, seed):
+    # MINI_NCCL_PULL=1 (csrc/schedule.h slot_owner / slot_region): every slot lives in the
+    # sender's scratch and the receiver loads it; same flags and credits, so the same bits and
+    # no deadlock under random interleavings, with several calls and iterations per pipeline
+    n = 2 + seed % 7
+    xs = O.random_inputs(n, 4000 + 17 * seed, "f32", seed=seed)
+    ref = O.allreduce(xs, slice_bytes=64)
+    got, _ = S.allreduce(xs, algo=algo, slice_bytes=64, channels=1 + seed % 3, slots=2 + seed % 2, calls=3,
+                         seed=seed, pull=1)
+    assert all(same_bits(g, e) for g, e in zip(got, ref))
