@@ -1,4 +1,4 @@
-"""Multi-process paths on the CPU (world_size 2, gloo): the bench harness's barrier /
+"""Multi-process paths on the CPU (world_size 2 and 4, gloo): the bench harness's barrier /
 max-over-ranks, the TCP bootstrap across processes, and the reference's C1 configuration
 (2-rank 127.0.0.1 TCP ring with AVX2 adds, oracle/ring_oracle.c) checked bit-exactly against
 the oracle -- the N > 1 host-side plumbing without a GPU."""
@@ -49,8 +49,8 @@ def _rank_main(rank, world, master_port, ring_port, boot_port, out_q):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
-@pytest.mark.parametrize("world", [2])
-def test_gloo_world2_harness_bootstrap_and_c1_ring(oracle_lib, sim_lib, world):
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_harness_bootstrap_and_host_ring(oracle_lib, sim_lib, world):
     import gpu_workers as GW
     ports = [GW.free_port() for _ in range(3)]
     out = GW.run_ranks(_rank_main, world, lambda r: (r, world, *ports), 120)
