@@ -26,6 +26,9 @@ def rows(path):
         return list(csv.DictReader(f))
 
 
+GRID_1GIB = (268435456 * 4) // 16  # threads of local_reduce_vec's exact grid over 1 GiB (one 16-B vector each)
+
+
 def ours(name):
     return "mnccl::" in name
 
@@ -57,7 +60,10 @@ def main():
     for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         for r in rows(os.path.join(src, sub, "run_counter_collection.csv")):
             if ours(r["Kernel_Name"]) and r["Counter_Name"] == counter:
-                per.setdefault((r["Kernel_Name"], counter), []).append(float(r["Counter_Value"]))
+                # per-launch bytes of the 1 GiB launch only (exact grid: 2^26 threads); smaller
+                # launches of the same kernel (e.g. bench's host-inclusive pieces) stay in the CSV
+                if int(r["Grid_Size"]) == GRID_1GIB:
+                    per.setdefault((r["Kernel_Name"], counter), []).append(float(r["Counter_Value"]))
                 pmc_rows.append([r["Kernel_Name"], r["Dispatch_Id"], r["Grid_Size"], r["Workgroup_Size"],
                                  r["VGPR_Count"], r["SGPR_Count"], counter, r["Counter_Value"]])
     with open(os.path.join(prof, f"{rnd}_n1_pmc.csv"), "w", newline="") as f:
