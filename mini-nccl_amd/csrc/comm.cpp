@@ -218,6 +218,9 @@ void Comm::tune() {
 
 Comm::~Comm() {
   hipSetDevice(device_);
+  // the last call may still run (stream-ordered mode): its kernel writes into the peers' scratch
+  // and mailboxes, which they free after the barrier below -- wait for it first
+  if (have_last_ && order_ev_) hipEventSynchronize(order_ev_);
   if (done_) hipEventSynchronize(done_);
   if (nranks_ > 1 && !peer_scratch_.empty()) {
     try {

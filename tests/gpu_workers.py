@@ -307,6 +307,34 @@ def huge_rank(rank, n, port, env, count, out_q):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def destroy_inflight_rank(rank, n, port, env, out_q):
+    """Stream-ordered calls still running when ncclCommDestroy is called: destroy waits for
+    them (their kernels write into the peers' memory, which the peers free right after), and
+    the results are complete once it returns."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        hip_rt.set_device(0)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        stream = hip_rt.Stream()
+        count = (64 << 20) // 4
+        buf = hip_rt.DeviceBuffer(count * 4)
+        buf.upload(np.ones(count, np.float32))
+        hip_rt.sync()
+        rcs = [comm.all_reduce(buf.ptr, buf.ptr, count, M.ncclFloat, M.ncclSum, stream.handle) for _ in range(3)]
+        rc_destroy = comm.destroy()  # no synchronisation before it
+        got = buf.download(np.float32, count)
+        stream.destroy()
+        buf.free()
+        body = (count // n) * n  # the count % n tail keeps this rank's input (mini_nccl.cu:69)
+        want = np.where(np.arange(count) < body, float(n) ** 3, 1.0).astype(np.float32)
+        out_q.put((rank, {"rcs": rcs, "destroy": rc_destroy, "bad": int((got != want).sum())}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
 def stall_rank(rank, n, port, env, call_allreduce, out_q):
     """Timeout test: rank 0 calls all-reduce, the other ranks never do."""
     try:

@@ -209,6 +209,17 @@ def test_allreduce_async_mode(dev):
     _run_allreduce(2, cases, env={"MINI_NCCL_BLOCKING": "0"})
 
 
+@pytest.mark.parametrize("algo", ["ring", "direct"])
+def test_destroy_waits_for_calls_in_flight(dev, algo):
+    port = GW.free_port()
+    env = {"MINI_NCCL_BLOCKING": "0", "MINI_NCCL_ALGO": algo, "MINI_NCCL_TUNE": "0", "MINI_NCCL_TIMEOUT_MS": "30000"}
+    out = GW.run_ranks(GW.destroy_inflight_rank, 3, lambda r: (r, 3, port, env), 180)
+    assert sorted(out) == [0, 1, 2], out
+    for r in range(3):
+        assert "error" not in out[r], out[r]["error"]
+        assert out[r]["rcs"] == [0, 0, 0] and out[r]["destroy"] == 0 and out[r]["bad"] == 0, out[r]
+
+
 def test_allreduce_reference_known_answers(dev):
     # perf_test.cpp: all ranks send 1.0 -> every element == nRanks (the oracle agrees)
     cases = [dict(_case(count=(16 << 20) // 4, seed=0), known="ones")]
