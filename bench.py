@@ -100,6 +100,7 @@ def cpu_baseline(budget_s=12.0):
         "sample": f"a += b over the full 1 GiB fp32 workload, {iters} timed passes after 1 warm pass "
                   f"(AVX2 _mm256_add_ps, {threads} threads); verify scan {'ok' if ok else 'FAILED'}",
         "single_thread_GBps": round(COUNT * 4 / t_st / 1e9, 3),
+        "nproc": os.cpu_count(),  # the whole machine's CPUs (the box's share is 16)
         "c1_tcp_ring": c1,
         "wall_s": round(time.time() - t_start, 1),
     }
@@ -121,7 +122,7 @@ def cpu_ring_baseline(n, budget_s=4.0):
     t1 = L.oracle_cpu_ring_threads_avx2(arr, n, cnt, 131072, 1)  # also the first touch
     iters = max(1, min(10, int(budget_s / max(t1, 1e-3))))
     t = L.oracle_cpu_ring_threads_avx2(arr, n, cnt, 131072, iters)
-    return {"value": round(cnt * 4 / t / 1e9, 3), "unit": "GB/s", "cores": n, "kind": "port",
+    return {"value": round(cnt * 4 / t / 1e9, 3), "unit": "GB/s", "cores": n, "nproc": os.cpu_count(), "kind": "port",
             "sample": f"{n}-thread in-process host ring (reference schedule, AVX2 adds), 256 MiB fp32 per rank, "
                       f"{iters} timed all-reduces after 1"}
 
