@@ -315,3 +315,41 @@ def test_count_beyond_int32(dev):
     for r in range(2):
         assert "error" not in out[r], out[r]["error"]
         assert out[r]["rc"] == 0 and out[r]["bad"] == 0, out[r]
+
+
+def _run_procs(cmds, env, timeout):
+    import subprocess
+    procs = [subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env) for c in cmds]
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            o, e = p.communicate()
+        outs.append((p.returncode, o, e))
+    return outs
+
+
+@pytest.mark.parametrize("prog", ["app", "perf_test"])
+def test_reference_programs_against_this_abi(dev, prog):
+    # the reference's own callers (src/main.cpp, tests/perf_test.cpp) rebuilt against
+    # include/mini_nccl_api.h + libmini_nccl.so (apps/), one process per rank on GPU 0 as the
+    # reference's README runs them: app checks 1.0 + 2.0 == 3.0 on 1 Mi floats (main.cpp:37-61),
+    # perf_test the all-ones known answer with its AVX2 scan (perf_test.cpp:81-134)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "apps", "bin", prog)
+    assert os.path.exists(exe), f"{exe} not built (make -C apps)"
+    env = dict(os.environ, MINI_NCCL_PORT=str(GW.free_port()), MINI_NCCL_PERF_DEVICE="0")
+    if prog == "app":
+        cmds = [[exe, str(r)] for r in range(2)]
+    else:
+        cmds = [[exe, str(r), "3", "--sizes", "1,16", "--iters", "3", "--warmup", "1"] for r in range(3)]
+    outs = _run_procs(cmds, env, 120)
+    for rc, o, e in outs:
+        assert rc == 0, (rc, o[-2000:], e[-2000:])
+    if prog == "app":
+        assert all("Result: [PASS]" in o for _, o, _ in outs)
+    else:
+        rows = [ln for ln in outs[0][1].splitlines() if ln.strip() and ln.strip()[0].isdigit()]
+        assert len(rows) == 2 and not any("FAIL" in ln for ln in rows), outs[0][1]
