@@ -29,15 +29,15 @@ typedef enum {
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
   mncclAlgoDirect = 1  /* every peer pushes its slice of chunk c straight to rank c over its
                           own xGMI link; c folds them in ring order c, c+1, ..., c-1 and
-                          pushes the result to every peer (from 3 ranks on, MINI_NCCL_ALGO=auto
-                          times both at init and keeps the faster) */
+                          pushes the result to every peer (MINI_NCCL_ALGO=auto: from 3 ranks
+                          on, when the ranks are on more than one GPU) */
 } mncclAlgo_t;
 
 typedef struct {
   int rank, nranks, device;
   size_t slice_bytes;     /* MINI_NCCL_SLICE_SIZE: bytes per channel message */
-  int window;             /* MINI_NCCL_WINDOW_SIZE: default number of workgroups (channels) */
-  int signal_batch;       /* MINI_NCCL_SIGNAL_BATCH (read and validated) */
+  int window;             /* MINI_NCCL_WINDOW_SIZE \ pipelines x slots <= WINDOW x SIGNAL_BATCH: the  */
+  int signal_batch;       /* MINI_NCCL_SIGNAL_BATCH / reference's bound on messages in flight per link */
   int channels;           /* workgroups of the persistent kernel; each wave is one pipeline */
   int slots;              /* scratch slots per channel (2 = the reference's double buffer) */
   int threads;            /* threads per workgroup */
@@ -46,9 +46,13 @@ typedef struct {
   int sys_fence;          /* MINI_NCCL_SYS_FENCE: system-scope release fence before each flag */
   double timeout_s;       /* MINI_NCCL_TIMEOUT_MS / 1000 */
   size_t scratch_bytes;   /* device scratch owned by this rank */
-  double tune_ms[2];      /* MINI_NCCL_ALGO=auto calibration at init (3+ ranks): ms per
+  double tune_ms[2];      /* MINI_NCCL_TUNE=1 calibration at init (auto algo, 3+ ranks): ms per
                              all-reduce of MINI_NCCL_TUNE_BYTES, ring / direct, max over
-                             ranks; 0 when not run (algo forced, MINI_NCCL_TUNE=0, 2 ranks) */
+                             ranks; 0 when not run (the default) */
+  int pipelines;          /* channels x threads / 64 */
+  int ranks_on_device;    /* ranks of this communicator on this rank's GPU (itself included) */
+  size_t slot_bytes;      /* largest payload per message (MINI_NCCL_SLICE_SIZE unless the
+                             scratch cap MINI_NCCL_SCRATCH_MB shrank it) */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,
@@ -58,6 +62,7 @@ ncclResult_t mncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError);
 
 ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info);
 
+/* every rank must make the same choice before its next all-reduce */
 ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo);
 
 /* Collective diagnostic: every rank streams `bytes` (0 = its whole scratch region) into the

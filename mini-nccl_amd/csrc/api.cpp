@@ -63,10 +63,9 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nRanks, int rank, const char
     Comm* c = new Comm(nRanks, rank, ip ? std::string(ip) : std::string("127.0.0.1"));
     *comm = reinterpret_cast<ncclComm_t>(c);
     return ncclSuccess;
-  } catch (const std::invalid_argument& e) {
-    fprintf(stderr, "[Mini-NCCL] Init Failed: %s\n", e.what());
-    return ncclInvalidUsage;
   } catch (const std::exception& e) {
+    // every init failure is ncclSystemError, as in the reference (api.cpp:62-65): also a
+    // configuration that differs between ranks, an unparsable MINI_NCCL_* value, nRanks > 16
     fprintf(stderr, "[Mini-NCCL] Init Failed: %s\n", e.what());
     return ncclSystemError;
   } catch (...) {
@@ -148,7 +147,6 @@ ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info) {
   info->slice_bytes = k.slice_size;
   info->window = k.window_size;
   info->signal_batch = k.signal_batch;
-  info->channels = k.channels;
   info->slots = k.slots;
   info->threads = k.threads;
   info->algo = c->algo();
@@ -158,9 +156,15 @@ ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info) {
   info->scratch_bytes = c->scratch_bytes();
   info->tune_ms[0] = c->tune_ms(0);
   info->tune_ms[1] = c->tune_ms(1);
+  info->channels = c->workgroups();
+  info->pipelines = c->wave_channels();
+  info->ranks_on_device = c->ranks_on_device();
+  info->slot_bytes = c->wave_slice();
   return ncclSuccess;
 }
 
+// Collective in effect: every rank must select the same schedule before its next call (the
+// schedules' messages share mailboxes and slots), as with any other communicator setting.
 ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo) {
   if (!comm) return ncclInvalidArgument;
   if (algo != mncclAlgoRing && algo != mncclAlgoDirect) return ncclInvalidArgument;

@@ -6,9 +6,12 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <random>
 #include <stdexcept>
 
 #include "schedule.h"
@@ -33,31 +36,90 @@ uint64_t host_hash() {
   return (uint64_t)std::hash<std::string>{}(std::string(h));
 }
 
+// Identifies this process among the ranks (pids repeat across pid namespaces, e.g. containers
+// of one pod sharing a hostname): random, drawn once per process.
+uint64_t process_nonce() {
+  static const uint64_t nonce = [] {
+    std::random_device rd;
+    uint64_t v = ((uint64_t)rd() << 32) ^ (uint64_t)rd();
+    v ^= (uint64_t)getpid() * 0x9E3779B97F4A7C15ull ^ (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    return v ? v : 1;
+  }();
+  return nonce;
+}
+
+// Physical identity of a device (PCI domain / bus / device): device ordinals differ between
+// processes that see different device sets, the PCI location does not.
+uint64_t pci_id(int dev) {
+  int dom = 0, bus = 0, d = 0;
+  if (hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, dev) != hipSuccess ||
+      hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dev) != hipSuccess ||
+      hipDeviceGetAttribute(&d, hipDeviceAttributePciDeviceId, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return ~0ull - (uint64_t)dev;
+  }
+  return ((uint64_t)(uint32_t)dom << 32) | ((uint64_t)(bus & 0xffff) << 16) | (uint64_t)(d & 0xffff);
+}
+
+// This process's ordinal of the device at PCI location `id`, or -1 if it is not visible here.
+int local_device_with_pci(uint64_t id) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  for (int d = 0; d < ndev; ++d)
+    if (pci_id(d) == id) return d;
+  return -1;
+}
+
+void enable_peer_access(int dev, int peer_dev, bool required) {
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, dev, peer_dev) != hipSuccess) (void)hipGetLastError();
+  if (!can) {
+    if (required)
+      throw std::runtime_error("device " + std::to_string(dev) + " cannot access peer device " + std::to_string(peer_dev));
+    return;
+  }
+  const hipError_t e = hipDeviceEnablePeerAccess(peer_dev, 0);
+  if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();
+    if (required) throw std::runtime_error(std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+  }
+  (void)hipGetLastError();
+}
+
 // Record every rank publishes once at init (the reference's RdmaInfo/DynamicMemInfo,
 // RDMATransport.h:25-48, reduced to what one node over HIP IPC needs).
 struct PeerInfo {
   uint32_t magic;
   int32_t rank, nranks, pid, device, pad0;
-  uint64_t host;
-  uint64_t slice, scratch_bytes, mbox_bytes;
+  uint64_t host, nonce, pci;  // nonce: same process <=> same nonce; pci: the physical GPU
+  uint64_t slice, scratch_bytes, mbox_bytes, scratch_cap;
   int32_t channels, slots, threads, abi;
-  uint64_t min_slice;
+  int32_t window, signal_batch, algo, tune;
+  uint64_t min_slice, tune_bytes;
   int32_t depth, overlap, pull, pad1;
   hipIpcMemHandle_t scratch_h, mbox_h;
   uint64_t scratch_ptr, mbox_ptr;  // raw addresses for ranks living in the same process
 };
-constexpr uint32_t kInfoMagic = 0x4d4e4931u;  // 'MNI1'
+constexpr uint32_t kInfoMagic = 0x4d4e4932u;  // 'MNI2'
 
 }  // namespace
 
 Comm::Comm(int nranks, int rank, const std::string& ip) : rank_(rank), nranks_(nranks) {
   cfg_ = Config::from_env();
-  // auto: the reference's ring for 2 ranks (one link either way); from 3 ranks on, the
-  // direct schedule, which gives the same bits but uses every xGMI link of the mesh
-  algo_ = cfg_.algo >= 0 ? cfg_.algo : (nranks >= 3 ? 1 : 0);
+  // auto: the reference's ring; from 3 ranks on GPUs of their own, the direct schedule (same
+  // bits, every xGMI link of the mesh) -- decided from the peers' devices in exchange_and_map
+  algo_ = cfg_.algo >= 0 ? cfg_.algo : 0;
   if (nranks > kMaxRanks) throw std::invalid_argument("nRanks > 16 is not supported on one node");
+  geo_ = pipeline_geometry(nranks, cfg_.channels, cfg_.threads, cfg_.window_size, cfg_.signal_batch, cfg_.slots,
+                           cfg_.slice_size, cfg_.scratch_cap);
   hip_check(hipGetDevice(&device_), "hipGetDevice");
-  if (cfg_.debug && rank == 0) fprintf(stderr, "[Config] Loaded: %s\n", cfg_.describe().c_str());
+  if (cfg_.debug && rank == 0)
+    fprintf(stderr, "[Config] Loaded: %s; geometry: %d workgroups x %d waves, slot %llu B, scratch %llu B\n",
+            cfg_.describe().c_str(), geo_.workgroups, geo_.waves, (unsigned long long)geo_.slot_bytes,
+            (unsigned long long)geo_.scratch_bytes);
   try {
     setup_device_resources();
     boot_.connect(rank, nranks, ip, cfg_.port, cfg_.bootstrap_timeout_ms / 1000.0);
@@ -73,23 +135,29 @@ void Comm::setup_device_resources() {
   // one channel per wave: `channels` workgroups x threads/64 waves; the reference's slice
   // (bytes per channel step) is split across the workgroup's waves
   const int C = wave_channels();
-  scratch_bytes_ = (size_t)nranks_ * scratch_region_bytes(C, cfg_.slots, wave_slice());
+  scratch_bytes_ = geo_.scratch_bytes;  // (n-1) peer regions, <= MINI_NCCL_SCRATCH_MB
   mbox_bytes_ = (size_t)mbox_words(nranks_, C) * sizeof(uint64_t);
-  if (nranks_ > 1) {
-    hip_check(hipExtMallocWithFlags((void**)&scratch_, scratch_bytes_, hipDeviceMallocUncached), "alloc scratch");
-    hip_check(hipExtMallocWithFlags((void**)&mbox_, mbox_bytes_, hipDeviceMallocUncached), "alloc mailbox");
-    hip_check(hipMemset(scratch_, 0, scratch_bytes_), "memset scratch");
-    hip_check(hipMemset(mbox_, 0, mbox_bytes_), "memset mailbox");
-    const size_t seq_bytes = (size_t)2 * nranks_ * C * sizeof(uint64_t);  // C = wave channels
-    hip_check(hipMalloc((void**)&pair_seq_, seq_bytes), "alloc pair_seq");
-    hip_check(hipMemset(pair_seq_, 0, seq_bytes), "memset pair_seq");
-  }
   hip_check(hipHostMalloc((void**)&h_ctl_, 4096, hipHostMallocMapped | hipHostMallocCoherent), "alloc ctl");
   memset(h_ctl_, 0, 4096);
   hip_check(hipHostGetDevicePointer((void**)&d_ctl_, h_ctl_, 0), "ctl device pointer");
   hip_check(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "event");
   hip_check(hipEventCreateWithFlags(&order_ev_, hipEventDisableTiming), "event");
-  hip_check(hipDeviceSynchronize(), "init sync");
+  if (nranks_ > 1) {
+    hip_check(hipExtMallocWithFlags((void**)&scratch_, scratch_bytes_, hipDeviceMallocUncached), "alloc scratch");
+    hip_check(hipExtMallocWithFlags((void**)&mbox_, mbox_bytes_, hipDeviceMallocUncached), "alloc mailbox");
+    const size_t seq_bytes = (size_t)2 * nranks_ * C * sizeof(uint64_t);  // C = wave channels
+    hip_check(hipMalloc((void**)&pair_seq_, seq_bytes), "alloc pair_seq");
+    // zeroed on a private stream: a device-wide sync (or the legacy null stream) would also wait
+    // for other communicators' persistent kernels in this process, which may be waiting for us
+    hipStream_t st = nullptr;
+    hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "init stream");
+    hipError_t e = hipMemsetAsync(scratch_, 0, scratch_bytes_, st);
+    if (e == hipSuccess) e = hipMemsetAsync(mbox_, 0, mbox_bytes_, st);
+    if (e == hipSuccess) e = hipMemsetAsync(pair_seq_, 0, seq_bytes, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    hipStreamDestroy(st);
+    hip_check(e, "zero scratch / mailbox / counters");
+  }
 }
 
 void Comm::exchange_and_map() {
@@ -105,14 +173,22 @@ void Comm::exchange_and_map() {
   me.pid = (int32_t)getpid();
   me.device = device_;
   me.host = host_hash();
+  me.nonce = process_nonce();
+  me.pci = pci_id(device_);
   me.slice = cfg_.slice_size;
   me.scratch_bytes = scratch_bytes_;
   me.mbox_bytes = mbox_bytes_;
+  me.scratch_cap = cfg_.scratch_cap;
   me.channels = cfg_.channels;
   me.slots = cfg_.slots;
   me.threads = cfg_.threads;
-  me.abi = 1;
+  me.abi = 2;
+  me.window = cfg_.window_size;
+  me.signal_batch = cfg_.signal_batch;
+  me.algo = cfg_.algo;
+  me.tune = cfg_.tune;
   me.min_slice = cfg_.min_slice;
+  me.tune_bytes = cfg_.tune_bytes;
   me.depth = cfg_.pipe_depth;
   me.overlap = cfg_.direct_overlap;
   me.pull = cfg_.pull;
@@ -128,11 +204,48 @@ void Comm::exchange_and_map() {
     if (p.magic != kInfoMagic || p.rank != q || p.nranks != nranks_)
       throw std::runtime_error("bootstrap: inconsistent rank records");
     if (p.host != me.host) throw std::runtime_error("rank " + std::to_string(q) + " is on another host: only one node is supported");
+    // every knob that shapes the kernels' geometry, message protocol or init sequence must agree
     if (p.slice != me.slice || p.channels != me.channels || p.slots != me.slots || p.threads != me.threads ||
-        p.min_slice != me.min_slice || p.depth != me.depth || p.overlap != me.overlap || p.pull != me.pull)
+        p.window != me.window || p.signal_batch != me.signal_batch || p.scratch_cap != me.scratch_cap ||
+        p.min_slice != me.min_slice || p.depth != me.depth || p.overlap != me.overlap || p.pull != me.pull ||
+        p.algo != me.algo || p.tune != me.tune || p.tune_bytes != me.tune_bytes || p.abi != me.abi)
       throw std::invalid_argument(
-          "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SLOTS / CHANNELS / THREADS / MIN_SLICE / PIPE_DEPTH / "
-          "DIRECT_OVERLAP / PULL differ between ranks");
+          "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SIGNAL_BATCH / SLOTS / CHANNELS / THREADS / SCRATCH_MB / MIN_SLICE / "
+          "PIPE_DEPTH / DIRECT_OVERLAP / PULL / ALGO / TUNE / TUNE_BYTES differ between ranks");
+  }
+  // the schedule for MINI_NCCL_ALGO=auto, the same on every rank (computed from the gathered
+  // records): from 3 ranks, `direct` when the ranks are on more than one GPU (each pair of an
+  // MI355X node has its own xGMI link; direct uses all of them, the ring one); `ring` when every
+  // rank shares one GPU (no links: the ring's neighbour-only coupling measured faster there,
+  // profiles/r2_direct_sweep_n4_same_gpu.txt) and at 2 ranks (one link either way)
+  bool one_device = true;
+  ranks_on_device_ = 0;
+  for (int q = 0; q < nranks_; ++q) {
+    if (all[(size_t)q].pci != all[0].pci) one_device = false;
+    if (all[(size_t)q].pci == me.pci) ++ranks_on_device_;
+  }
+  if (cfg_.algo < 0) algo_ = (nranks_ >= 3 && !one_device) ? 1 : 0;
+  // Rank PROCESSES sharing this GPU: a persistent kernel waits for its peers' kernels, so all of
+  // them must be resident at once; the GPU's scheduler maps a bounded number of processes and
+  // hardware queues together, beyond which it time-slices and every hand-off waits for a turn
+  // (measured on MI355X: 8 processes x 2 queues each run at full rate, 8 x 4 -- HIP's default
+  // GPU_MAX_HW_QUEUES -- are ~200x slower, and a 9th GPU process stalls them).
+  {
+    std::vector<uint64_t> procs;
+    for (int q = 0; q < nranks_; ++q)
+      if (all[(size_t)q].pci == me.pci && std::find(procs.begin(), procs.end(), all[(size_t)q].nonce) == procs.end())
+        procs.push_back(all[(size_t)q].nonce);
+    const char* hq = std::getenv("GPU_MAX_HW_QUEUES");
+    const int queues = hq && *hq ? std::max(1, atoi(hq)) : 4;
+    bool first_here = true;  // warn once per GPU: from its lowest rank
+    for (int q = 0; q < rank_; ++q)
+      if (all[(size_t)q].pci == me.pci) first_here = false;
+    if (procs.size() > 1 && procs.size() * (size_t)queues > 16 && first_here)
+      fprintf(stderr,
+              "[Mini-NCCL] warning: %zu rank processes share GPU %d with up to %d hardware queues each; the "
+              "all-reduce needs every rank's kernel resident at once -- keep processes x GPU_MAX_HW_QUEUES <= 16 "
+              "(and no other process using this GPU), or calls will stall on time-slicing\n",
+              procs.size(), device_, queues);
   }
   for (int q = 0; q < nranks_; ++q) {
     if (q == rank_) {
@@ -141,19 +254,19 @@ void Comm::exchange_and_map() {
       continue;
     }
     const PeerInfo& p = all[(size_t)q];
-    if (p.pid == me.pid) {  // same process (e.g. threads of one test): plain pointers
+    if (p.nonce == me.nonce) {
+      // same process (threads of one program, one rank each): plain pointers; another device's
+      // memory needs peer access from this one
+      if (p.device != device_) enable_peer_access(device_, p.device, true);
       peer_scratch_[(size_t)q] = (char*)(uintptr_t)p.scratch_ptr;
       peer_mbox_[(size_t)q] = (uint64_t*)(uintptr_t)p.mbox_ptr;
       continue;
     }
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) == hipSuccess && p.device != device_ && p.device < ndev) {
-      int can = 0;
-      if (hipDeviceCanAccessPeer(&can, device_, p.device) == hipSuccess && can) {
-        hipError_t e = hipDeviceEnablePeerAccess(p.device, 0);
-        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
-      }
-    }
+    // another process: its GPU by PCI location (ordinals differ between processes that see
+    // different device sets); if it is visible here, enable peer access to it explicitly,
+    // otherwise the IPC mapping's lazy peer access does it
+    const int pd = local_device_with_pci(p.pci);
+    if (pd >= 0 && pd != device_) enable_peer_access(device_, pd, false);
     void* ps = nullptr;
     void* pm = nullptr;
     hip_check(hipIpcOpenMemHandle(&ps, p.scratch_h, hipIpcMemLazyEnablePeerAccess), "ipc open scratch");
@@ -166,11 +279,11 @@ void Comm::exchange_and_map() {
   boot_.barrier();
 }
 
-// MINI_NCCL_ALGO=auto from 3 ranks on: both schedules give the same bits, and which one is
-// faster depends on the links (on the xGMI mesh `direct` spreads over n-1 links, on a shared
-// device the ring's fewer bytes per hop can win).  Time one in-place all-reduce of
-// MINI_NCCL_TUNE_BYTES per rank with each (one warm-up, three timed), take the max over ranks
-// (allgather over the bootstrap, so every rank computes the same choice) and keep the faster.
+// MINI_NCCL_ALGO=auto with MINI_NCCL_TUNE=1 (opt-in; the default decides from the devices, see
+// exchange_and_map), from 3 ranks on: both schedules give the same bits.  Time one in-place
+// all-reduce of MINI_NCCL_TUNE_BYTES per rank with each (one warm-up, three timed), take the max
+// over ranks (allgather over the bootstrap, so every rank computes the same choice) and keep the
+// faster.
 void Comm::tune() {
   const size_t count = cfg_.tune_bytes / 4;
   float* buf = nullptr;
@@ -180,9 +293,9 @@ void Comm::tune() {
   bool ok = true;
   try {
     hip_check(hipMalloc((void**)&buf, count * 4), "tune alloc");
-    hip_check(hipMemset(buf, 0, count * 4), "tune memset");
-    hip_check(hipDeviceSynchronize(), "tune sync");
     hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "tune stream");
+    hip_check(hipMemsetAsync(buf, 0, count * 4, st), "tune memset");
+    hip_check(hipStreamSynchronize(st), "tune sync");
     hip_check(hipEventCreate(&e0), "tune event");
     hip_check(hipEventCreate(&e1), "tune event");
     for (int a = 0; a < 2 && ok; ++a) {
@@ -299,17 +412,29 @@ ncclResult_t Comm::async_error() {
   return ncclSuccess;
 }
 
-// Host side of the reference's watchdog (mini_nccl.cu:200-214): wait for the stream; after
-// the kernel's own timeout plus a grace period, raise the abort word the kernel polls.
-ncclResult_t Comm::wait_for(hipStream_t stream) {
+// Host side of the reference's watchdog (mini_nccl.cu:200-214): wait for the stream; once this
+// call's kernel has started (it writes its sequence number into the start word, so work the
+// caller queued before it never counts), after the kernel's own timeout plus a grace period,
+// raise the abort word the kernel polls.  Work ahead of the kernel on the stream is the caller's
+// and is waited for without a deadline (the abort word could not reach it anyway).
+ncclResult_t Comm::wait_for(hipStream_t stream, uint32_t seq) {
   hip_check(hipEventRecord(done_, stream), "event record");
-  const double t0 = now_s();
+  double t0 = -1.0;
   const double limit = cfg_.timeout_ms / 1000.0 + 2.0;
   bool aborted = false;
   for (int spins = 0;; ++spins) {
     hipError_t q = hipEventQuery(done_);
     if (q == hipSuccess) break;
     if (q != hipErrorNotReady) hip_check(q, "stream query");
+    if (t0 < 0.0) {
+      const uint32_t started = __atomic_load_n(&h_ctl_[2], __ATOMIC_ACQUIRE);
+      if (seq != 0 && (int32_t)(started - seq) < 0) {
+        if (spins < 2000) sched_yield();
+        else usleep(100);
+        continue;
+      }
+      t0 = now_s();
+    }
     const double el = now_s() - t0;
     if (!aborted && el > limit) {
       fprintf(stderr, "[Watchdog] TIMEOUT DETECTED on rank %d! Aborting GPU kernels...\n", rank_);
@@ -344,21 +469,28 @@ Comm::Reach Comm::reach(const void* p, const void** kernel_ptr) const {
   return Reach::kStaged;
 }
 
-void Comm::ensure_stage(size_t bytes) {
+// Stream-ordered on the call's stream (which already waits for this communicator's previous
+// call, see allreduce): no device-wide sync, which would also wait for other communicators'
+// persistent kernels in this process.
+void Comm::ensure_stage(size_t bytes, hipStream_t stream) {
   if (stage_bytes_ >= bytes) return;
   if (stage_) {
-    hip_check(hipDeviceSynchronize(), "stage regrow sync");  // earlier calls may still use it
-    hip_check(hipFree(stage_), "free stage");
+    hip_check(hipFreeAsync(stage_, stream), "free stage");
     stage_ = nullptr;
     stage_bytes_ = 0;
   }
   const size_t want = (bytes + ((size_t)1 << 20) - 1) & ~(((size_t)1 << 20) - 1);
-  hip_check(hipMalloc((void**)&stage_, want), "alloc stage");
+  hip_check(hipMallocAsync((void**)&stage_, want, stream), "alloc stage");
   stage_bytes_ = want;
 }
 
+// Host wait for this communicator's last call (its kernel writes into the peers' memory)
+void Comm::wait_previous_call() {
+  if (have_last_) hip_check(hipEventSynchronize(order_ev_), "wait for the previous call");
+}
+
 void Comm::launch_ring_or_direct(const void* send, void* recv, size_t chunk_bytes, int dtype, int op,
-                                 hipStream_t stream) {
+                                 hipStream_t stream, uint32_t seq) {
   const int n = nranks_;
   CollParams p;
   memset(&p, 0, sizeof p);
@@ -383,6 +515,8 @@ void Comm::launch_ring_or_direct(const void* send, void* recv, size_t chunk_byte
   }
   p.status = d_ctl_;
   p.host_abort = d_ctl_ + 1;
+  p.started = d_ctl_ + 2;
+  p.call_seq = seq;
   p.timeout_ticks = (uint64_t)(cfg_.timeout_ms * 1e5);  // s_memrealtime runs at 100 MHz
   p.sys_fence = cfg_.sys_fence;
   p.direct_overlap = cfg_.direct_overlap;
@@ -391,8 +525,8 @@ void Comm::launch_ring_or_direct(const void* send, void* recv, size_t chunk_byte
   // straddle 16-byte boundaries on the local side; each message's last len % 16 bytes go
   // element by element); element-wise path otherwise (2-byte types with odd chunks)
   const bool vec = (((uintptr_t)send | (uintptr_t)recv) % 4 == 0) && (chunk_bytes % 4 == 0);
-  hipError_t e = algo_ == 1 ? launch_direct(dtype, op, vec, cfg_.channels, cfg_.threads, p, stream)
-                            : launch_ring(dtype, op, vec, cfg_.channels, cfg_.threads, p, stream);
+  hipError_t e = algo_ == 1 ? launch_direct(dtype, op, vec, geo_.workgroups, cfg_.threads, p, stream)
+                            : launch_ring(dtype, op, vec, geo_.workgroups, cfg_.threads, p, stream);
   hip_check(e, "kernel launch");
 }
 
@@ -426,6 +560,7 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     hip_check(hipStreamWaitEvent(stream, order_ev_, 0), "order after previous call");
 
   const int n = nranks_;
+  uint32_t seq = 0;  // this call's kernel (0: the call launches none)
   const size_t chunk = n > 0 ? count / (size_t)n : 0;  // mini_nccl.cu:69
   const size_t chunk_bytes = chunk * (size_t)esz;
   if (n == 1 || chunk == 0) {
@@ -446,7 +581,7 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
         if (cur_dev != device_) hipSetDevice(cur_dev);
         return ncclInvalidUsage;
       }
-      ensure_stage(bytes);
+      ensure_stage(bytes, stream);
       if (rs == Reach::kStaged) {
         hip_check(hipMemcpyAsync(stage_, send, bytes, hipMemcpyDefault, stream), "stage in");
         ksend = stage_;
@@ -461,7 +596,9 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
       hip_check(hipMemcpyAsync((char*)krecv + body, (const char*)ksend + body, bytes - body, hipMemcpyDefault,
                                stream),
                 "tail copy");
-    launch_ring_or_direct(ksend, krecv, chunk_bytes, dtype, op, stream);
+    seq = ++call_seq_;
+    if (seq == 0) seq = ++call_seq_;  // 0 = "no kernel" (wait_for)
+    launch_ring_or_direct(ksend, krecv, chunk_bytes, dtype, op, stream, seq);
     if (rr == Reach::kStaged) hip_check(hipMemcpyAsync(recv, stage_, bytes, hipMemcpyDefault, stream), "stage out");
   }
   if (!capturing) {
@@ -470,7 +607,7 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     have_last_ = true;
   }
   if (cur_dev != device_) hipSetDevice(cur_dev);
-  if (cfg_.blocking && cap == hipStreamCaptureStatusNone) return wait_for(stream);
+  if (cfg_.blocking && cap == hipStreamCaptureStatusNone) return wait_for(stream, seq);
   return ncclSuccess;
 }
 
@@ -483,22 +620,26 @@ ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gb
   all_peers &= 1;
   const size_t region = scratch_region_bytes(wave_channels(), cfg_.slots, wave_slice());
   if (bytes == 0 || bytes > region) bytes = region;  // the probe writes this rank's region at each peer
+  int cur_dev = -1;
+  hip_check(hipGetDevice(&cur_dev), "hipGetDevice");
   hip_check(hipSetDevice(device_), "hipSetDevice");
+  wait_previous_call();  // no all-reduce of this communicator may still be writing slots
+  hipStream_t st;
+  hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "probe stream");
   char* src = nullptr;
   hip_check(hipMalloc((void**)&src, bytes), "probe alloc");
-  hip_check(hipMemset(src, 0x5a, bytes), "probe memset");
+  hip_check(hipMemsetAsync(src, 0x5a, bytes, st), "probe memset");
   std::vector<char*> dst;
   for (int k = 1; k < nranks_; ++k) {
     const int d = (rank_ + k) % nranks_;
-    dst.push_back(peer_scratch_[(size_t)d] + (size_t)rank_ * region);
+    // in push mode this rank's region at d is where d receives from this rank
+    dst.push_back(peer_scratch_[(size_t)d] + (size_t)region_index(d, rank_) * region);
     if (!all_peers) break;
   }
-  hipStream_t st;
-  hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "probe stream");
   hipEvent_t e0, e1;
   hip_check(hipEventCreate(&e0), "event");
   hip_check(hipEventCreate(&e1), "event");
-  hip_check(hipDeviceSynchronize(), "probe sync");
+  hip_check(hipStreamSynchronize(st), "probe sync");
   boot_.barrier();  // every rank idle and launching together
   hip_check(launch_link_probe(src, dst.data(), (int)dst.size(), bytes, form, pull, st), "probe warm-up");
   hip_check(hipEventRecord(e0, st), "event");
@@ -514,6 +655,7 @@ ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gb
   hipEventDestroy(e1);
   hipStreamDestroy(st);
   hipFree(src);
+  if (cur_dev != device_) hipSetDevice(cur_dev);
   return ncclSuccess;
 }
 

@@ -12,6 +12,7 @@
 #include "config.h"
 #include "kernels.h"
 #include "mini_nccl_api.h"
+#include "schedule.h"
 
 namespace mnccl {
 
@@ -32,33 +33,42 @@ class Comm {
   const Config& config() const { return cfg_; }
   int algo() const { return algo_; }
   void set_algo(int a) { algo_ = a; }
-  // calibration of MINI_NCCL_ALGO=auto (max over ranks, ms per call; 0 = not run)
+  // calibration of MINI_NCCL_ALGO=auto with MINI_NCCL_TUNE=1 (max over ranks, ms per call; 0 = not run)
   double tune_ms(int a) const { return tune_ms_[a & 1]; }
+  // rank processes / communicators whose GPU is this rank's GPU (this rank included)
+  int ranks_on_device() const { return ranks_on_device_; }
   ncclResult_t async_error();
   // Collective: every rank writes `bytes` into the next rank's scratch (all_peers = 0) or into
   // every peer's scratch at once (1), `iters` times; *gbps = bytes per second per link
   // direction (max over nothing: this rank's own time).  No all-reduce may be in flight.
   ncclResult_t link_probe(int all_peers, size_t bytes, int iters, double* gbps);
   size_t scratch_bytes() const { return scratch_bytes_; }
-  // kernel geometry: one pipeline per wave, each moving MINI_NCCL_SLICE_SIZE bytes per message
-  int wave_channels() const { return cfg_.channels * (cfg_.threads / 64); }
-  uint64_t wave_slice() const { return cfg_.slice_size; }
+  // kernel geometry (schedule.h pipeline_geometry): one pipeline per wave, each moving up to
+  // slot_bytes (MINI_NCCL_SLICE_SIZE unless the scratch cap shrank it) per message
+  int workgroups() const { return geo_.workgroups; }
+  int wave_channels() const { return geo_.workgroups * geo_.waves; }
+  uint64_t wave_slice() const { return geo_.slot_bytes; }
 
  private:
   void setup_device_resources();
   void release();
   void exchange_and_map();
   void tune();
-  ncclResult_t wait_for(hipStream_t stream);
+  ncclResult_t wait_for(hipStream_t stream, uint32_t seq);
   enum class Reach { kDevice, kMapped, kStaged };
   Reach reach(const void* p, const void** kernel_ptr) const;
-  void ensure_stage(size_t bytes);
-  void launch_ring_or_direct(const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream);
+  void ensure_stage(size_t bytes, hipStream_t stream);
+  void launch_ring_or_direct(const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
+                             uint32_t seq);
+  void wait_previous_call();
   ncclResult_t check_status();
 
   int rank_, nranks_, device_ = 0;
   Config cfg_;
+  Geometry geo_;
   int algo_ = 0;
+  int ranks_on_device_ = 1;
+  uint32_t call_seq_ = 0;        // kernel launches of this communicator (the kernel's start word)
   double tune_ms_[2] = {0.0, 0.0};
   Bootstrap boot_;
 
@@ -67,7 +77,7 @@ class Comm {
   uint64_t* mbox_ = nullptr;     // uncached device memory: READY / CREDIT / ABORT words
   size_t mbox_bytes_ = 0;
   uint64_t* pair_seq_ = nullptr; // [2][n][C]: per (peer, channel) tx / rx message counters (device)
-  uint32_t* h_ctl_ = nullptr;    // host-mapped: [0] status, [1] abort request
+  uint32_t* h_ctl_ = nullptr;    // host-mapped: [0] status, [1] abort request, [2] last started call
   uint32_t* d_ctl_ = nullptr;    // device view of h_ctl_
 
   std::vector<char*> peer_scratch_;

@@ -30,6 +30,8 @@ Config Config::from_env() {
   if (slice <= 0) slice = 1024;  // Config.h:50 maps 0 -> 1024
   slice &= ~15LL;                // whole 16-byte vectors per message (slicing never changes results)
   if (slice < 16) slice = 16;
+  // message lengths and slot offsets are 32-bit in the kernels (buffer resources): bound it
+  if (slice > (long long)kMaxSlice) slice = (long long)kMaxSlice;
   c.slice_size = (size_t)slice;
   c.window_size = (int)env_int("MINI_NCCL_WINDOW_SIZE", 64);
   if (c.window_size <= 0) c.window_size = 1;  // Config.h:51
@@ -40,14 +42,15 @@ Config Config::from_env() {
   // the message it is about to overwrite) -- a cycle; tests/test_schedule.py shows it
   if (c.slots < 2) c.slots = 2;
   if (c.slots > 64) c.slots = 64;
+  // workgroups; each wave is one pipeline.  0 = derived per communicator (Comm::geometry: one
+  // pipeline per CU, bounded by WINDOW x SIGNAL_BATCH messages in flight and the scratch cap)
   c.channels = (int)env_int("MINI_NCCL_CHANNELS", 0);
-  // workgroups; each wave is one pipeline.  Default 4 x WINDOW one-wave workgroups (256 at the
-  // reference's WINDOW 64): one pipeline per CU of the 256, so no two pipelines share a CU's
-  // L1 / address path (2 ranks on one GPU: 372 -> 791 GB/s against 64 four-wave workgroups,
-  // profiles/r1_geometry_sweep.txt)
-  if (c.channels <= 0) c.channels = 4 * c.window_size;
-  if (c.channels < 1) c.channels = 1;
+  if (c.channels < 0) c.channels = 0;
   if (c.channels > 1024) c.channels = 1024;
+  long long cap_mb = env_int("MINI_NCCL_SCRATCH_MB", 512);
+  if (cap_mb < 1) cap_mb = 1;
+  if (cap_mb > (64LL << 10)) cap_mb = 64LL << 10;
+  c.scratch_cap = (size_t)cap_mb << 20;
   c.threads = (int)env_int("MINI_NCCL_THREADS", 64);
   if (c.threads < 64) c.threads = 64;
   if (c.threads > kMaxThreads) c.threads = kMaxThreads;  // the kernels' launch bound (kernels.h)
@@ -68,7 +71,7 @@ Config Config::from_env() {
   if (c.pipe_depth < 1) c.pipe_depth = 1;
   c.direct_overlap = env_int("MINI_NCCL_DIRECT_OVERLAP", 1) != 0;
   c.pull = env_int("MINI_NCCL_PULL", 0) != 0;
-  c.tune = env_int("MINI_NCCL_TUNE", 1) != 0;
+  c.tune = env_int("MINI_NCCL_TUNE", 0) != 0;
   long long tb = env_int("MINI_NCCL_TUNE_BYTES", 64LL << 20);
   if (tb < (1LL << 20)) tb = 1LL << 20;
   c.tune_bytes = (size_t)(tb & ~255LL);
@@ -82,11 +85,11 @@ Config Config::from_env() {
 }
 
 std::string Config::describe() const {
-  char b[320];
+  char b[384];
   snprintf(b, sizeof b,
-           "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, algo=%s, blocking=%d, "
-           "sys_fence=%d, min_slice=%zu, depth=%d, pull=%d, tune=%d, stage_host=%d, timeout=%.0f ms, port=%d",
-           slice_size, window_size, signal_batch, slots, channels, threads,
+           "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, scratch_cap=%zu MiB, algo=%s, "
+           "blocking=%d, sys_fence=%d, min_slice=%zu, depth=%d, pull=%d, tune=%d, stage_host=%d, timeout=%.0f ms, port=%d",
+           slice_size, window_size, signal_batch, slots, channels, threads, scratch_cap >> 20,
            algo < 0 ? "auto" : algo ? "direct" : "ring", blocking,
            sys_fence, min_slice, pipe_depth, pull, tune, stage_host, timeout_ms, port);
   return b;

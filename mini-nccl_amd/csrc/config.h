@@ -10,11 +10,12 @@ namespace mnccl {
 struct Config {
   // reference knobs, same names and defaults (Config.h:29-51)
   size_t slice_size = 128 * 1024;  // MINI_NCCL_SLICE_SIZE (bytes per channel message; 0 -> 1024)
-  int window_size = 64;            // MINI_NCCL_WINDOW_SIZE (workgroups of the persistent kernel)
-  int signal_batch = 16;           // MINI_NCCL_SIGNAL_BATCH (validated)
+  int window_size = 64;            // MINI_NCCL_WINDOW_SIZE \  messages in flight per link <=
+  int signal_batch = 16;           // MINI_NCCL_SIGNAL_BATCH / WINDOW x SIGNAL_BATCH (see Comm::geometry)
   // this build's knobs
   int slots = 2;                   // MINI_NCCL_SLOTS   scratch slots per channel (>= 2; 2 = double buffer)
-  int channels = 0;                // MINI_NCCL_CHANNELS workgroups (0 -> 4 x window_size)
+  int channels = 0;                // MINI_NCCL_CHANNELS workgroups (0 -> derived, Comm::geometry)
+  size_t scratch_cap = 512u << 20; // MINI_NCCL_SCRATCH_MB cap on this rank's uncached scratch
   int threads = 64;                // MINI_NCCL_THREADS threads per workgroup (one pipeline per wave)
   int algo = -1;                   // MINI_NCCL_ALGO    auto (-1) | ring (0) | direct (1)
   int blocking = 1;                // MINI_NCCL_BLOCKING host waits for the stream (reference behaviour)
@@ -23,7 +24,7 @@ struct Config {
   int pipe_depth = 1;              // MINI_NCCL_PIPE_DEPTH slices per pipeline targeted for small calls
   int direct_overlap = 1;          // MINI_NCCL_DIRECT_OVERLAP next iteration's raw pushes before this one's results
   int pull = 0;                    // MINI_NCCL_PULL   1: slots in the sender's scratch, loaded over the link
-  int tune = 1;                    // MINI_NCCL_TUNE   auto algo: time both schedules at init (n >= 3)
+  int tune = 0;                    // MINI_NCCL_TUNE   1: auto algo times both schedules at init (n >= 3)
   size_t tune_bytes = 64u << 20;   // MINI_NCCL_TUNE_BYTES per-rank buffer of that calibration
   int stage_host = 0;              // MINI_NCCL_STAGE_HOST pinned host buffers: 0 = kernel maps them, 1 = staged copy
   double timeout_ms = 10000.0;     // MINI_NCCL_TIMEOUT_MS (reference watchdog: 10 s)

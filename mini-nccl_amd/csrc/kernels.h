@@ -27,6 +27,8 @@ struct CollParams {
   uint64_t* peer_mbox[16]; // peers' mailboxes (IPC-mapped), indexed by rank
   uint32_t* status;        // host-mapped status word (kStatus* bits)
   const uint32_t* host_abort;  // host-mapped abort request
+  uint32_t* started;       // host-mapped start word: the kernel writes call_seq when it begins
+  uint32_t call_seq;       // this launch's sequence number (Comm::wait_for's deadline starts here)
   uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
   int32_t sys_fence;       // system-scope release fence before each ready flag
   int32_t direct_overlap;  // direct: next iteration's raw pushes before this one's results

@@ -317,6 +317,11 @@ __device__ __forceinline__ void abort_peers(const CollParams& p, int C, int a, i
   st_sys(p.peer_mbox[b] + mbox_abort(p.n, C), 1ull);
 }
 
+// the host watchdog's deadline starts when the kernel does (Comm::wait_for): one posted write
+__device__ __forceinline__ void signal_start(const CollParams& p) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) st_sys32(p.started, p.call_seq);
+}
+
 // channel geometry: one channel per wave
 struct WaveId {
   int lane, wv, w, C;
@@ -334,6 +339,7 @@ __device__ __forceinline__ WaveId wave_id() {
 // ---------------------------------------------------------------- ring kernel
 template <typename T, int OPC, bool VEC>
 __global__ void __launch_bounds__(kMaxThreads) ring_kernel(CollParams p) {
+  signal_start(p);
   const WaveId id = wave_id();
   const int lane = id.lane, w = id.w, C = id.C;
   const int n = p.n, r = p.rank, K = p.nslots;
@@ -502,6 +508,7 @@ constexpr int kPushU = MNCCL_PUSH_U;
 
 template <typename T, int OPC, bool VEC>
 __global__ void __launch_bounds__(kMaxThreads) direct_kernel(CollParams p) {
+  signal_start(p);
   const WaveId id = wave_id();
   const int lane = id.lane, w = id.w, C = id.C, wv = id.wv;
   const int n = p.n, r = p.rank, K = p.nslots;

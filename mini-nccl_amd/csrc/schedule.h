@@ -51,6 +51,11 @@ struct RingOp {
 // launch bound lets the compiler give a pipeline's wave up to 512 VGPRs instead of the 128 a
 // 1024-thread bound allows (the direct fold spilled at 128); one wave per workgroup is the default.
 constexpr int kMaxThreads = 256;
+// Largest message payload / slot stride (MINI_NCCL_SLICE_SIZE is clamped to it): message
+// lengths and slot offsets are 32-bit in the kernels' buffer resources.
+constexpr uint64_t kMaxSlice = 256ull << 20;
+// Default pipelines of the persistent kernels: one per CU of the 256.
+constexpr int kDefaultPipelines = 256;
 
 MNCCL_HD int mod_n(int a, int n) { return ((a % n) + n) % n; }
 
@@ -130,6 +135,61 @@ MNCCL_HD uint64_t effective_slice(uint64_t chunk_bytes, int C, uint64_t slice, u
   return want < slice ? want : slice;
 }
 
+// Scratch layout: one region per PEER rank (n - 1 of them: the owner never sends to itself),
+// [C][slots][slice_bytes] each.  region_index maps a peer rank q != owner to its region.
+MNCCL_HD uint64_t scratch_region_bytes(int C, int slots, uint64_t slice_bytes) { return (uint64_t)C * slots * slice_bytes; }
+MNCCL_HD int region_index(int owner, int q) { return q < owner ? q : q - 1; }
+MNCCL_HD uint64_t scratch_slot_off(int C, int slots, uint64_t slice_bytes, int region, int w, uint64_t seq) {
+  return (uint64_t)region * scratch_region_bytes(C, slots, slice_bytes) +
+         ((uint64_t)w * slots + (seq % (uint64_t)slots)) * slice_bytes;
+}
+
+// Kernel geometry of one communicator (Comm, and the CPU tests through the simulator library):
+// a pure function of the rank-uniform config and n, so every rank computes the same.
+//  * workgroups: MINI_NCCL_CHANNELS if set; otherwise one pipeline per CU (256), bounded by the
+//    reference's in-flight bound: WINDOW pending signalled requests, each covering SIGNAL_BATCH
+//    messages (mini_nccl.cu:119,144,167), i.e. pipelines x slots <= WINDOW x SIGNAL_BATCH
+//    messages in flight per link (64 x 16 = 1024 >= 256 x 2 at the defaults);
+//  * then the scratch cap: (n-1) regions x pipelines x slots x slot <= cap (fewer pipelines, the
+//    payload per message stays MINI_NCCL_SLICE_SIZE; only if one workgroup cannot fit does the
+//    slot shrink, to whole KiB).
+struct Geometry {
+  int workgroups;
+  int waves;             // per workgroup (threads / 64): pipelines = workgroups x waves
+  uint64_t slot_bytes;   // slot stride and largest payload per message
+  uint64_t scratch_bytes;
+};
+MNCCL_HD Geometry pipeline_geometry(int n, int channels, int threads, int window, int signal_batch, int slots,
+                                    uint64_t slice, uint64_t cap) {
+  Geometry g;
+  g.waves = threads / 64 > 0 ? threads / 64 : 1;
+  if (slots < 1) slots = 1;
+  if (channels > 0) {
+    g.workgroups = channels;
+  } else {
+    uint64_t inflight = (uint64_t)(window > 0 ? window : 1) * (uint64_t)(signal_batch > 0 ? signal_batch : 1);
+    uint64_t P = inflight / (uint64_t)slots;
+    if (P > (uint64_t)kDefaultPipelines) P = kDefaultPipelines;
+    uint64_t wg = P / (uint64_t)g.waves;
+    g.workgroups = wg < 1 ? 1 : (int)wg;
+  }
+  g.slot_bytes = slice;
+  const uint64_t regions = n > 1 ? (uint64_t)(n - 1) : 0;
+  if (regions) {
+    const uint64_t per_wg = (uint64_t)g.waves * (uint64_t)slots * slice * regions;
+    const uint64_t max_wg = cap / per_wg;
+    if (max_wg < 1) {
+      g.workgroups = 1;
+      uint64_t s = (cap / ((uint64_t)g.waves * (uint64_t)slots * regions)) & ~(uint64_t)1023;
+      g.slot_bytes = s < 1024 ? 1024 : s;
+    } else if ((uint64_t)g.workgroups > max_wg) {
+      g.workgroups = (int)max_wg;
+    }
+  }
+  g.scratch_bytes = regions * scratch_region_bytes(g.workgroups * g.waves, slots, g.slot_bytes);
+  return g;
+}
+
 // Mailbox layout (uint64 words, one 128-byte line per flag):
 //   READY(src, w)  : written by rank src when its message for this rank landed
 //   CREDIT(dst, w) : written by rank dst when it has consumed a message from this rank
@@ -140,19 +200,12 @@ MNCCL_HD uint64_t mbox_credit(int n, int C, int dst, int w) { return ((uint64_t)
 MNCCL_HD uint64_t mbox_abort(int n, int C) { return (uint64_t)2 * n * C * kFlagStride; }
 MNCCL_HD uint64_t mbox_words(int n, int C) { return mbox_abort(n, C) + kFlagStride; }
 
-// Scratch layout: region per source rank, [C][slots][slice_bytes] each.
-MNCCL_HD uint64_t scratch_region_bytes(int C, int slots, uint64_t slice_bytes) { return (uint64_t)C * slots * slice_bytes; }
-MNCCL_HD uint64_t scratch_slot_off(int C, int slots, uint64_t slice_bytes, int src, int w, uint64_t seq) {
-  return (uint64_t)src * scratch_region_bytes(C, slots, slice_bytes) +
-         ((uint64_t)w * slots + (seq % (uint64_t)slots)) * slice_bytes;
-}
-
 // Where message `seq` from rank `src` to rank `dst` (pipeline w) lives.  Push (default): in the
 // receiver's scratch, region src -- the sender's stores cross the link.  Pull
 // (MINI_NCCL_PULL=1): in the sender's own scratch, region dst -- the receiver's loads cross the
 // link.  Flags, credits and sequence numbers are the same either way.
 MNCCL_HD int slot_owner(int pull, int src, int dst) { return pull ? src : dst; }
-MNCCL_HD int slot_region(int pull, int src, int dst) { return pull ? dst : src; }
+MNCCL_HD int slot_region(int pull, int src, int dst) { return region_index(slot_owner(pull, src, dst), pull ? dst : src); }
 
 // Kernel status bits (host-mapped status word)
 enum : uint32_t { kStatusTimeout = 1u, kStatusHostAbort = 2u, kStatusRemoteAbort = 4u };

@@ -183,6 +183,16 @@ void mnccl_direct_phase_at(uint32_t j, uint32_t iters, int overlap, int* phase, 
 uint64_t mnccl_effective_slice(uint64_t chunk_bytes, int channels, uint64_t slice, uint64_t min_slice, int depth) {
   return effective_slice(chunk_bytes, channels, slice, min_slice, depth);
 }
+// csrc/schedule.h pipeline_geometry (what Comm allocates and launches): out = {workgroups,
+// waves, slot_bytes, scratch_bytes}
+void mnccl_pipeline_geometry(int n, int channels, int threads, int window, int signal_batch, int slots,
+                             uint64_t slice, uint64_t cap, uint64_t* out) {
+  const Geometry g = pipeline_geometry(n, channels, threads, window, signal_batch, slots, slice, cap);
+  out[0] = (uint64_t)g.workgroups;
+  out[1] = (uint64_t)g.waves;
+  out[2] = g.slot_bytes;
+  out[3] = g.scratch_bytes;
+}
 
 // Runs `calls` consecutive all-reduces (send -> recv, fp32) on n simulated ranks with the
 // GPU kernels' protocol; call i uses schedule (algo >> i) & 1 (so schedules can alternate
@@ -205,7 +215,8 @@ int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, 
   W.iters = (uint32_t)((W.nslices + (uint64_t)channels - 1) / (uint64_t)channels);
   W.send.assign(send, send + n);
   W.recv.assign(recv, recv + n);
-  W.scratch.assign((size_t)n, std::vector<char>((size_t)n * scratch_region_bytes(channels, slots, slice_bytes)));
+  // n - 1 regions per rank, exactly as Comm allocates (schedule.h region_index)
+  W.scratch.assign((size_t)n, std::vector<char>((size_t)(n > 1 ? n - 1 : 1) * scratch_region_bytes(channels, slots, slice_bytes)));
   W.mbox.assign((size_t)n, std::vector<uint64_t>((size_t)mbox_words(n, channels), 0));
   W.tx_seq.assign((size_t)n, std::vector<uint64_t>((size_t)n * channels, 0));
   W.rx_seq.assign((size_t)n, std::vector<uint64_t>((size_t)n * channels, 0));

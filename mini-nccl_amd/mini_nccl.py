@@ -48,6 +48,7 @@ class CommInfo(ctypes.Structure):
         ("channels", ctypes.c_int), ("slots", ctypes.c_int), ("threads", ctypes.c_int),
         ("algo", ctypes.c_int), ("blocking", ctypes.c_int), ("sys_fence", ctypes.c_int),
         ("timeout_s", ctypes.c_double), ("scratch_bytes", ctypes.c_size_t), ("tune_ms", ctypes.c_double * 2),
+        ("pipelines", ctypes.c_int), ("ranks_on_device", ctypes.c_int), ("slot_bytes", ctypes.c_size_t),
     ]
 
 

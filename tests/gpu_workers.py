@@ -46,8 +46,11 @@ def make_inputs(n, count, dtype, seed, special):
     return xs
 
 
-def allreduce_rank(rank, n, port, cases, env, out_q):
-    """Run `cases` on one communicator; report per-case mismatch counts."""
+def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
+    """Run `cases` on one communicator; report per-case mismatch counts.  With a barrier (a
+    multiprocessing.Barrier shared by the rank processes), every rank finishes its host-side
+    preparation (inputs, oracle, uploads) before any rank enters a call, so the watchdog
+    measures the library, not the harness's per-process skew."""
     try:
         os.environ.update(env)
         os.environ["MINI_NCCL_PORT"] = str(port)
@@ -92,6 +95,8 @@ def allreduce_rank(rank, n, port, cases, env, out_q):
                     xs = make_inputs(n, count, dtype, seed + 1000 * c, case.get("special", False))
                     exp = O.allreduce(xs, dtype, op, inplace=inplace)[rank]
                 send.upload(xs[rank], off)
+                if barrier is not None:
+                    barrier.wait(120)
                 if skew:
                     time.sleep(float(rng.uniform(0, skew)) / 1000.0)
                 rc = comm.all_reduce(send.ptr + off, recv.ptr + off, count, code, O.OPS[op], stream.handle)
@@ -361,15 +366,161 @@ def stall_rank(rank, n, port, env, call_allreduce, out_q):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
-def run_ranks(target, n, args_for_rank, timeout):
-    """Spawn n rank processes, collect one result each; kill stragglers at the deadline."""
+def delayed_start_rank(rank, n, port, env, delay_s, out_q):
+    """Work queued ahead of the all-reduce on its stream (a stream wait on a host word that a
+    timer thread raises after delay_s) must not count against the watchdog: the host deadline
+    starts when the kernel does.  Blocking call, MINI_NCCL_TIMEOUT_MS well below delay_s."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import threading
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        hip_rt.set_device(0)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        st = hip_rt.Stream()
+        count = (1 << 20) + 3
+        xs = O.random_inputs(n, count, "f32", seed=77)
+        send, recv = hip_rt.DeviceBuffer(count * 4), hip_rt.DeviceBuffer(count * 4)
+        send.upload(xs[rank])
+        gate = hip_rt.HostBuffer(64)
+        gate.fill_byte(0)
+        st.wait_value32(gate.ptr, 1)
+        t = threading.Timer(delay_s, lambda: gate.upload(np.array([1], np.uint32)))
+        t.start()
+        t0 = time.time()
+        rc = comm.all_reduce(send.ptr, recv.ptr, count, M.ncclFloat, M.ncclSum, st.handle)
+        secs = time.time() - t0
+        t.join()
+        st.sync()
+        got = recv.download(np.float32, count)
+        bad = int((got.view(np.uint32) != O.allreduce(xs)[rank].view(np.uint32)).sum())
+        res = {"rc": rc, "secs": secs, "bad": bad, "async": comm.async_error()}
+        send.free()
+        recv.free()
+        gate.free()
+        st.destroy()
+        res["destroy"] = comm.destroy()
+        out_q.put((rank, res))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
+def local_reduce_case(dtype, op, count, offset):
+    """mncclLocalReduce on seeded inputs vs the oracle's element-wise op (in the calling
+    process); returns (mismatches, first index, got, expected) for the test's message."""
+    import hip_rt
+    import mini_nccl as M
+    import oracle_api as O
+    hip_rt.set_device(0)
+    code, npd = O.DTYPES[dtype]
+    a, b = make_inputs(2, count, dtype, seed=count + 7, special=op in ("max", "min"))
+    exp = O.reduce(a, b, dtype, op)
+    esz = np.dtype(npd).itemsize
+    off = offset * esz if offset else 0
+    da, db, dc = (hip_rt.DeviceBuffer(count * esz + off) for _ in range(3))
+    try:
+        da.upload(a, off)
+        db.upload(b, off)
+        rc = M.local_reduce(dc.ptr + off, da.ptr + off, db.ptr + off, count, code, O.OPS[op], 0)
+        if rc != M.ncclSuccess:
+            return (-1, -1, f"ncclResult {rc}", "")
+        hip_rt.sync()
+        got = dc.download(npd, count, off)
+        bad, first = compare(got, exp, dtype, op in ("sum", "prod"))
+        return (bad, first, repr(got[first]) if bad else "", repr(exp[first]) if bad else "")
+    finally:
+        for x in (da, db, dc):
+            x.free()
+
+
+def local_reduce_in_place_large():
+    """256 MiB fp32 a <- a + b in place, bit-exact vs the oracle; returns mismatches."""
+    import hip_rt
+    import mini_nccl as M
+    import oracle_api as O
+    hip_rt.set_device(0)
+    count = 64 << 20
+    a, b = make_inputs(2, count, "f32", seed=5, special=False)
+    exp = O.reduce(a, b, "f32", "sum")
+    da, db = hip_rt.DeviceBuffer(a.nbytes), hip_rt.DeviceBuffer(b.nbytes)
+    try:
+        da.upload(a)
+        db.upload(b)
+        if M.local_reduce(da.ptr, da.ptr, db.ptr, count, M.ncclFloat, M.ncclSum, 0) != 0:
+            return -1
+        hip_rt.sync()
+        return int((da.download(np.float32, count).view(np.uint32) != exp.view(np.uint32)).sum())
+    finally:
+        da.free()
+        db.free()
+
+
+def device_count_probe(out_q):
+    import hip_rt
+    out_q.put((0, {"count": hip_rt.device_count()}))
+
+
+def _serve(conn):
+    """Worker loop: (function name, args) in, ("ok", result) / ("error", traceback) out."""
+    while True:
+        msg = conn.recv()
+        if msg is None:
+            break
+        name, args = msg
+        try:
+            conn.send(("ok", globals()[name](*args)))
+        except Exception:
+            conn.send(("error", traceback.format_exc()))
+    conn.close()
+
+
+class Worker:
+    """A long-lived GPU process for single-process GPU tests.  The pytest process itself never
+    touches the GPU: the GPU's scheduler maps at most 8 processes at once, and a 9th process
+    holding queues (the test runner) makes 8 co-located rank processes time-slice, which stalls
+    the persistent all-reduce kernels.  close() ends the process and frees its queues."""
+
+    def __init__(self):
+        import multiprocessing as mp
+        ctx = mp.get_context("forkserver")
+        self.conn, child = ctx.Pipe()
+        self.proc = ctx.Process(target=_serve, args=(child,))
+        self.proc.start()
+        child.close()
+
+    def call(self, name, *args, timeout=300):
+        self.conn.send((name, args))
+        if not self.conn.poll(timeout):
+            raise TimeoutError(f"{name}{args} did not finish in {timeout} s")
+        status, val = self.conn.recv()
+        if status != "ok":
+            raise RuntimeError(val)
+        return val
+
+    def close(self):
+        try:
+            self.conn.send(None)
+        except Exception:
+            pass
+        self.proc.join(30)
+        if self.proc.is_alive():
+            self.proc.kill()
+            self.proc.join(5)
+
+
+def run_ranks(target, n, args_for_rank, timeout, barrier=False):
+    """Spawn n rank processes, collect one result each; kill stragglers at the deadline.
+    barrier=True passes a shared multiprocessing.Barrier(n) as the target's `barrier` kwarg."""
     import multiprocessing as mp
     # forkserver: children fork from a server started before this process touched the GPU
     # (conftest starts it), so no child is forked from a GPU-initialised process and
     # nothing exec()s after HIP init
     ctx = mp.get_context("forkserver")
     q = ctx.Queue()
-    procs = [ctx.Process(target=target, args=args_for_rank(r) + (q,)) for r in range(n)]
+    kw = {"barrier": ctx.Barrier(n)} if barrier else {}
+    procs = [ctx.Process(target=target, args=args_for_rank(r) + (q,), kwargs=kw) for r in range(n)]
     for p in procs:
         p.start()
     out = {}

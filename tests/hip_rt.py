@@ -40,6 +40,8 @@ def lib():
         _hip.hipGraphLaunch.argtypes = [vp, vp]
         _hip.hipGraphExecDestroy.argtypes = [vp]
         _hip.hipGraphDestroy.argtypes = [vp]
+        _hip.hipStreamWaitValue32.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint, ctypes.c_uint32]
+        _hip.hipStreamWaitValue32.restype = i
         for f in ("hipStreamBeginCapture", "hipStreamEndCapture", "hipGraphInstantiate", "hipGraphLaunch",
                   "hipGraphExecDestroy", "hipGraphDestroy"):
             getattr(_hip, f).restype = i
@@ -153,6 +155,11 @@ class Stream:
 
     def sync(self):
         check(lib().hipStreamSynchronize(self.handle), "hipStreamSynchronize")
+
+    def wait_value32(self, ptr, value):
+        """Block the stream (on the GPU) until the 32-bit word at `ptr` (pinned host memory) is
+        >= value (hipStreamWaitValueGte)."""
+        check(lib().hipStreamWaitValue32(self.handle, ptr, value, 0, 0xFFFFFFFF), "hipStreamWaitValue32")
 
     def destroy(self):
         if self.handle:

@@ -26,6 +26,7 @@ def load():
         L.mnccl_effective_slice.restype = u64
         L.mnccl_bootstrap_selftest.argtypes = [i, i, ctypes.c_char_p, i, i]
         L.mnccl_config_describe.argtypes = [ctypes.c_char_p, i]
+        L.mnccl_pipeline_geometry.argtypes = [i, i, i, i, i, i, u64, u64, ctypes.POINTER(u64)]
         _lib = L
     return _lib
 
@@ -61,6 +62,14 @@ def config_describe(env=None):
     buf = ctypes.create_string_buffer(512)
     rc = load().mnccl_config_describe(buf, 512)
     return rc, buf.value.decode()
+
+
+def pipeline_geometry(n, channels=0, threads=64, window=64, signal_batch=16, slots=2, slice_bytes=128 << 10,
+                      cap=512 << 20):
+    """csrc/schedule.h pipeline_geometry: what a communicator allocates and launches."""
+    out = (ctypes.c_uint64 * 4)()
+    load().mnccl_pipeline_geometry(n, channels, threads, window, signal_batch, slots, slice_bytes, cap, out)
+    return {"workgroups": out[0], "waves": out[1], "slot_bytes": out[2], "scratch_bytes": out[3]}
 
 
 def effective_slice(chunk_bytes, channels, slice_bytes, min_slice, depth=1):

@@ -136,14 +136,19 @@ def test_config_from_env(sim_lib, monkeypatch):
             monkeypatch.delenv(k)
     rc, s = S.config_describe()
     assert rc == 0
-    # reference defaults (Config.h:29-47): 128 KiB, 64, 16; one-wave workgroups = 4 x window
-    assert "SLICE_SIZE=131072 B" in s and "WINDOW=64" in s and "BATCH=16" in s and "channels=256" in s
+    # reference defaults (Config.h:29-47): 128 KiB, 64, 16; workgroups derived per communicator
+    # (channels=0, schedule.h pipeline_geometry); no auto-tune at init; 512 MiB scratch cap
+    assert "SLICE_SIZE=131072 B" in s and "WINDOW=64" in s and "BATCH=16" in s and "channels=0" in s
     assert "algo=auto" in s and "threads=64" in s and "sys_fence=0" in s and "min_slice=1024" in s
+    assert "tune=0" in s and "scratch_cap=512 MiB" in s
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", "0")       # Config.h:50: 0 -> 1024
     monkeypatch.setenv("MINI_NCCL_WINDOW_SIZE", "-3")     # Config.h:51: <= 0 -> 1
     monkeypatch.setenv("MINI_NCCL_SLOTS", "1")            # clamped to 2 (deadlock-free minimum)
     rc, s = S.config_describe()
-    assert "SLICE_SIZE=1024 B" in s and "WINDOW=1" in s and "slots=2" in s and "channels=4" in s
+    assert "SLICE_SIZE=1024 B" in s and "WINDOW=1" in s and "slots=2" in s and "channels=0" in s
+    monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", str(8 << 30))  # 32-bit message lengths: clamped
+    rc, s = S.config_describe()
+    assert rc == 0 and f"SLICE_SIZE={256 << 20} B" in s
     monkeypatch.setenv("MINI_NCCL_ALGO", "direct")
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", "100")     # rounded down to whole 16-byte vectors
     rc, s = S.config_describe()
@@ -154,3 +159,34 @@ def test_config_from_env(sim_lib, monkeypatch):
     monkeypatch.setenv("MINI_NCCL_ALGO", "tree")
     rc, s = S.config_describe()
     assert rc == -1 and "MINI_NCCL_ALGO" in s
+
+
+def test_pipeline_geometry(sim_lib):
+    import sim_api as S
+    MiB = 1 << 20
+    # defaults: one pipeline per CU (256), (n-1) peer regions of 256 x 2 x 128 KiB
+    g = S.pipeline_geometry(8)
+    assert g == {"workgroups": 256, "waves": 1, "slot_bytes": 128 << 10, "scratch_bytes": 7 * 256 * 2 * (128 << 10)}
+    assert g["scratch_bytes"] == 448 * MiB
+    assert S.pipeline_geometry(2)["scratch_bytes"] == 64 * MiB
+    assert S.pipeline_geometry(1)["scratch_bytes"] == 0
+    # WINDOW x SIGNAL_BATCH bounds the messages in flight per link (mini_nccl.cu:119,144,167):
+    # pipelines x slots <= WINDOW x SIGNAL_BATCH; at WINDOW >= 32 the 256-pipeline default binds
+    assert [S.pipeline_geometry(8, window=w)["workgroups"] for w in (16, 32, 64)] == [128, 256, 256]
+    assert S.pipeline_geometry(8, window=1)["workgroups"] == 8
+    assert S.pipeline_geometry(8, window=16, signal_batch=1)["workgroups"] == 8
+    assert S.pipeline_geometry(8, window=64, threads=256)["workgroups"] == 64  # 4 waves each
+    # the scratch cap: BASELINE C4's SLICE = 1 MiB at WINDOW 64 keeps 1 MiB messages, fewer pipelines
+    for sl in (64 << 10, 128 << 10, 256 << 10, 1 << 20):
+        for w in (16, 32, 64):
+            g = S.pipeline_geometry(8, window=w, slice_bytes=sl)
+            assert g["scratch_bytes"] <= 512 * MiB and g["slot_bytes"] == sl, (sl, w, g)
+    assert S.pipeline_geometry(8, slice_bytes=1 << 20)["workgroups"] == 36
+    # MINI_NCCL_CHANNELS is honoured up to the cap
+    assert S.pipeline_geometry(4, channels=64)["workgroups"] == 64
+    assert S.pipeline_geometry(8, channels=1024)["workgroups"] == 292
+    # a slice so large that one workgroup cannot fit: the slot shrinks (whole KiB), never the cap
+    g = S.pipeline_geometry(8, slice_bytes=256 * MiB)
+    assert g["workgroups"] == 1 and g["slot_bytes"] % 1024 == 0 and g["scratch_bytes"] <= 512 * MiB
+    g = S.pipeline_geometry(8, cap=16 * MiB, slice_bytes=1 << 20)
+    assert g["workgroups"] == 1 and g["scratch_bytes"] <= 16 * MiB

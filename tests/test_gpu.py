@@ -9,6 +9,7 @@
 * error paths: watchdog timeout -> ncclInternalError and a sticky error afterwards.
 """
 import os
+import time
 
 import numpy as np
 import pytest
@@ -24,57 +25,42 @@ OPS = ["sum", "prod", "max", "min"]
 
 @pytest.fixture(scope="module")
 def dev(nccl_lib, oracle_lib):
-    import hip_rt
-    if hip_rt.device_count() < 1:
+    # the device check runs in a child: this (pytest) process must hold no GPU queues, or the
+    # 8-rank tests would put 9 processes on the GPU (see gpu_workers.Worker)
+    out = GW.run_ranks(GW.device_count_probe, 1, lambda r: (), 120)
+    if not out or out[0]["count"] < 1:
         pytest.fail("no HIP device visible: the -m gpu suite must run on the MI355X box")
-    hip_rt.set_device(0)
-    return hip_rt
+    return True
 
 
-@pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("op", OPS)
-@pytest.mark.parametrize("count,offset", [(1 << 20, 0), (100003, 0), (4099, 4), (17, 2), (65539, 1), (1 << 16, 3)])
-def test_local_reduce_parity(dev, dtype, op, count, offset):
-    import mini_nccl as M
-    code, npd = O.DTYPES[dtype]
-    a, b = GW.make_inputs(2, count, dtype, seed=count + 7, special=op in ("max", "min"))
-    exp = O.reduce(a, b, dtype, op)
-    esz = np.dtype(npd).itemsize
-    off = offset * esz if offset else 0
-    da, db, dc = (dev.DeviceBuffer(count * esz + off) for _ in range(3))
-    da.upload(a, off)
-    db.upload(b, off)
-    rc = M.local_reduce(dc.ptr + off, da.ptr + off, db.ptr + off, count, code, O.OPS[op], 0)
-    assert rc == M.ncclSuccess
-    dev.sync()
-    got = dc.download(npd, count, off)
-    bad, first = GW.compare(got, exp, dtype, op in ("sum", "prod"))
-    assert bad == 0, f"{bad} mismatches, first at {first}: got {got[first]!r} expected {exp[first]!r}"
-    for x in (da, db, dc):
-        x.free()
+class TestLocalReduce:
+    """mncclLocalReduce (the scatter-reduce element-wise kernel) in one worker process that ends
+    with the class, before the multi-rank tests start."""
+
+    @pytest.fixture(scope="class")
+    def worker(self, dev):
+        w = GW.Worker()
+        yield w
+        w.close()
+
+    @pytest.mark.parametrize("dtype", DTYPES)
+    @pytest.mark.parametrize("op", OPS)
+    @pytest.mark.parametrize("count,offset", [(1 << 20, 0), (100003, 0), (4099, 4), (17, 2), (65539, 1), (1 << 16, 3)])
+    def test_local_reduce_parity(self, worker, dtype, op, count, offset):
+        bad, first, got, exp = worker.call("local_reduce_case", dtype, op, count, offset)
+        assert bad == 0, f"{bad} mismatches, first at {first}: got {got} expected {exp}"
+
+    def test_local_reduce_in_place_large(self, worker):
+        assert worker.call("local_reduce_in_place_large") == 0
 
 
-def test_local_reduce_in_place_large(dev):
-    import mini_nccl as M
-    count = 64 << 20  # 256 MiB fp32
-    a, b = GW.make_inputs(2, count, "f32", seed=5, special=False)
-    exp = O.reduce(a, b, "f32", "sum")
-    da, db = dev.DeviceBuffer(a.nbytes), dev.DeviceBuffer(b.nbytes)
-    da.upload(a)
-    db.upload(b)
-    assert M.local_reduce(da.ptr, da.ptr, db.ptr, count, M.ncclFloat, M.ncclSum, 0) == 0
-    dev.sync()
-    assert np.array_equal(da.download(np.float32, count).view(np.uint32), exp.view(np.uint32))
-    da.free()
-    db.free()
-
-
-def _run_allreduce(n, cases, env=None, timeout=300):
+def _run_allreduce(n, cases, env=None, timeout=300, barrier=True):
     port = GW.free_port()
-    # every case sets its schedule explicitly: no auto-tune run at init
+    # every case sets its schedule explicitly; the ranks line up before each call (barrier)
     e = {"MINI_NCCL_TIMEOUT_MS": "30000", "MINI_NCCL_TUNE": "0"}
     e.update(env or {})
-    out = GW.run_ranks(GW.allreduce_rank, n, lambda r: (r, n, port, cases, e), timeout)
+    out = GW.run_ranks(GW.allreduce_rank, n, lambda r: (r, n, port, cases, e), timeout,
+                       barrier=barrier)
     assert len(out) == n, f"only ranks {sorted(out)} reported (timeout?)"
     for r in range(n):
         assert "error" not in out[r], f"rank {r}:\n{out[r]['error']}"
@@ -138,20 +124,33 @@ def test_skewed_ranks_varying_data(dev, algo, blocking):
     _run_allreduce(4, cases, env={"MINI_NCCL_BLOCKING": blocking})
 
 
-def test_auto_tune_picks_the_faster_schedule(dev):
-    # MINI_NCCL_ALGO=auto from 3 ranks: both schedules timed at init (max over ranks, every rank
-    # sees the same numbers), the faster kept; forcing a schedule or 2 ranks skips it
+def test_auto_schedule_from_devices_no_init_allreduce(dev):
+    # MINI_NCCL_ALGO=auto (default): the schedule comes from the gathered device records, no
+    # all-reduce runs at init (tune_ms stays 0); every rank on one GPU -> ring at any n
     port = GW.free_port()
-    env = {"MINI_NCCL_TUNE_BYTES": str(8 << 20)}
+    out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {}), 120)
+    assert all("error" not in out[r] for r in range(3)), out
+    for r in range(3):
+        i = out[r]["info"]
+        assert i["tune_ms"] == [0.0, 0.0] and i["algo"] == 0 and i["ranks_on_device"] == 3, i
+        assert i["channels"] == 256 and i["pipelines"] == 256 and i["slot_bytes"] == 128 << 10
+        assert i["scratch_bytes"] == 2 * 256 * 2 * (128 << 10)  # (n-1) peer regions
+    port = GW.free_port()
+    out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {"MINI_NCCL_ALGO": "direct"}), 120)
+    assert out[0]["info"]["tune_ms"] == [0.0, 0.0] and out[0]["info"]["algo"] == 1
+
+
+def test_auto_tune_opt_in_picks_the_faster_schedule(dev):
+    # MINI_NCCL_TUNE=1: both schedules timed at init (max over ranks, every rank sees the same
+    # numbers), the faster kept
+    port = GW.free_port()
+    env = {"MINI_NCCL_TUNE": "1", "MINI_NCCL_TUNE_BYTES": str(8 << 20)}
     out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, env), 120)
     assert all("error" not in out[r] for r in range(3)), out
     infos = [out[r]["info"] for r in range(3)]
     t = infos[0]["tune_ms"]
     assert t[0] > 0 and t[1] > 0 and all(i["tune_ms"] == t for i in infos)
     assert all(i["algo"] == (1 if t[1] <= t[0] else 0) for i in infos)
-    port = GW.free_port()
-    out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {"MINI_NCCL_ALGO": "direct"}), 120)
-    assert out[0]["info"]["tune_ms"] == [0.0, 0.0] and out[0]["info"]["algo"] == 1
 
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
@@ -164,16 +163,35 @@ def test_sys_fence_on(dev, algo):
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
 def test_allreduce_8_ranks(dev, algo):
-    # the 8-GPU node's rank count, all on GPU 0: every pair of the mesh is exercised
-    # one call per test (each call can meet a scheduling stall, see below): direct -- the 8-GPU
-    # default -- in f32 out of place, ring in bf16 in place
-    cases = ([_case(count=(1 << 20) + 5, algo=algo, seed=8)] if algo == 1 else
-             [_case(dtype="bf16", count=(1 << 19) + 3, algo=algo, inplace=True, seed=9)])
-    # 8 processes time-share one GPU here: their queues are not always resident together, so a
-    # rank's persistent kernel can wait a whole scheduling round for a peer's (1 s in one run,
-    # 42 s in another): fewer workgroups and a watchdog far above that (the 8-GPU node gives
-    # each rank its own GPU and the default 10 s)
-    _run_allreduce(8, cases, env={"MINI_NCCL_CHANNELS": "8", "MINI_NCCL_TIMEOUT_MS": "180000"}, timeout=700)
+    # the 8-GPU node's rank count, all on GPU 0 at the library's default geometry (256
+    # pipelines): every pair of the mesh exercised; BASELINE C3 (fp32) and C5 (fp16, bf16) on
+    # order-sensitive seeded data, bit-exact vs the oracle
+    cases = [_case(count=(1 << 20) + 5, algo=algo, seed=8),                              # C3 fp32
+             _case(dtype="f16", count=(1 << 20) + 3, algo=algo, inplace=True, seed=9),  # C5 fp16
+             _case(dtype="bf16", count=(1 << 19) + 3, algo=algo, inplace=True, seed=10),  # C5 bf16
+             _case(count=8 * 4099 + 7, algo=algo, calls=2, seed=11)]
+    _run_allreduce(8, cases, timeout=600)
+
+
+def test_allreduce_8_ranks_c3_ring_128mib(dev):
+    # C3's schedule (the reference's ring) in fp32 at 8 ranks on 128 MiB per rank: 16 MiB chunks,
+    # every one of the 256 pipelines busy (64 KiB payloads), bit-exact vs the oracle
+    cases = [_case(count=8 * (4 << 20) + 3, algo=0, seed=1234)]
+    _run_allreduce(8, cases, timeout=600)
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("slice_kib", [64, 256, 1024])
+def test_allreduce_slice_points(dev, slice_kib, n, algo):
+    # BASELINE C4's MINI_NCCL_SLICE_SIZE points (64K / 256K / 1M; 128K is the default everywhere
+    # else) with full-size payloads: 16 workgroups so that each pipeline moves >= 3 full slices
+    # per chunk plus a ragged one; fp32 and fp16, order-sensitive data, bit-exact vs the oracle
+    sl = slice_kib << 10
+    chunk_el = 16 * 3 * sl // 4 + 12345
+    cases = [_case(count=n * chunk_el + 1, algo=algo, seed=60 + slice_kib),
+             _case(dtype="f16", count=n * (chunk_el // 2) + 3, algo=algo, inplace=True, seed=61 + slice_kib)]
+    _run_allreduce(n, cases, env={"MINI_NCCL_SLICE_SIZE": str(sl), "MINI_NCCL_CHANNELS": "16"}, timeout=600)
 
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
@@ -284,14 +302,37 @@ def test_single_rank_is_copy_only(dev):
     _run_allreduce(1, cases)
 
 
-@pytest.mark.parametrize("knob,values", [("MINI_NCCL_SLICE_SIZE", ("131072", "65536")), ("MINI_NCCL_PULL", ("0", "1"))])
-def test_mismatched_config_is_invalid_usage(dev, knob, values):
+@pytest.mark.parametrize("knob,values", [("MINI_NCCL_SLICE_SIZE", ("131072", "65536")), ("MINI_NCCL_PULL", ("0", "1")),
+                                         ("MINI_NCCL_ALGO", ("ring", "direct")), ("MINI_NCCL_TUNE", ("0", "1")),
+                                         ("MINI_NCCL_WINDOW_SIZE", ("64", "16"))])
+def test_mismatched_config_is_system_error(dev, knob, values):
+    # every init failure is ncclSystemError, as in the reference (api.cpp:62-65)
     import mini_nccl as M
     port = GW.free_port()
     env = {0: {knob: values[0]}, 1: {knob: values[1]}}
     out = GW.run_ranks(GW.init_rank, 2, lambda r: (r, 2, port, env), 120)
     assert sorted(out) == [0, 1], out
-    assert out[0]["rc"] == M.ncclInvalidUsage and out[1]["rc"] == M.ncclInvalidUsage
+    assert out[0]["rc"] == M.ncclSystemError and out[1]["rc"] == M.ncclSystemError
+
+
+def test_unparsable_knob_is_system_error(dev):
+    import mini_nccl as M
+    port = GW.free_port()
+    out = GW.run_ranks(GW.init_rank, 1, lambda r: (r, 1, port, {0: {"MINI_NCCL_SLICE_SIZE": "12x"}}), 60)
+    assert out[0]["rc"] == M.ncclSystemError, out
+
+
+def test_watchdog_deadline_starts_with_the_kernel(dev):
+    # 6 s of work queued ahead of the call on its stream, a 3 s kernel watchdog: the host's
+    # deadline (timeout + 2 s) must count from the kernel's start, not from the call
+    port = GW.free_port()
+    env = {"MINI_NCCL_TIMEOUT_MS": "3000", "MINI_NCCL_ALGO": "ring"}
+    out = GW.run_ranks(GW.delayed_start_rank, 2, lambda r: (r, 2, port, env, 6.0), 120)
+    assert sorted(out) == [0, 1], out
+    for r in range(2):
+        assert "error" not in out[r], out[r]["error"]
+        assert out[r]["rc"] == 0 and out[r]["bad"] == 0 and out[r]["async"] == 0, out[r]
+        assert out[r]["secs"] >= 5.5 and out[r]["destroy"] == 0, out[r]
 
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
@@ -331,25 +372,40 @@ def _run_procs(cmds, env, timeout):
     return outs
 
 
-@pytest.mark.parametrize("prog", ["app", "perf_test"])
+@pytest.mark.parametrize("prog", ["app", "app_device", "perf_test", "perf_test_host", "perf_test_8"])
 def test_reference_programs_against_this_abi(dev, prog):
     # the reference's own callers (src/main.cpp, tests/perf_test.cpp) rebuilt against
     # include/mini_nccl_api.h + libmini_nccl.so (apps/), one process per rank on GPU 0 as the
     # reference's README runs them: app checks 1.0 + 2.0 == 3.0 on 1 Mi floats (main.cpp:37-61),
     # perf_test the all-ones known answer with its AVX2 scan (perf_test.cpp:81-134)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    exe = os.path.join(root, "apps", "bin", prog)
+    exe = os.path.join(root, "apps", "bin", "app" if prog.startswith("app") else "perf_test")
     assert os.path.exists(exe), f"{exe} not built (make -C apps)"
     env = dict(os.environ, MINI_NCCL_PORT=str(GW.free_port()), MINI_NCCL_PERF_DEVICE="0")
+    t0 = time.time()
     if prog == "app":
-        cmds = [[exe, str(r)] for r in range(2)]
+        cmds = [[exe, str(r)] for r in range(2)]  # pinned host buffer, as main.cpp:35
+    elif prog == "app_device":
+        cmds = [[exe, str(r), "--device-buffer"] for r in range(2)]
+    elif prog == "perf_test_host":
+        # the reference's own buffers: cudaHostAlloc'd send / recv handed to ncclAllReduce
+        cmds = [[exe, str(r), "3", "--mode", "host", "--sizes", "1,16", "--iters", "3", "--warmup", "1"]
+                for r in range(3)]
+    elif prog == "perf_test_8":
+        # `perf_test <r> 8` x 8 on GPU 0 with the default environment (the reference's topology,
+        # perf_test.cpp:46): completes within seconds
+        env = {k: v for k, v in env.items() if not k.startswith("MINI_NCCL_") or k == "MINI_NCCL_PORT"}
+        env["MINI_NCCL_PERF_DEVICE"] = "0"
+        cmds = [[exe, str(r), "8", "--sizes", "1,16", "--iters", "3", "--warmup", "1"] for r in range(8)]
     else:
         cmds = [[exe, str(r), "3", "--sizes", "1,16", "--iters", "3", "--warmup", "1"] for r in range(3)]
     outs = _run_procs(cmds, env, 120)
     for rc, o, e in outs:
         assert rc == 0, (rc, o[-2000:], e[-2000:])
-    if prog == "app":
+    if prog.startswith("app"):
         assert all("Result: [PASS]" in o for _, o, _ in outs)
     else:
+        if prog == "perf_test_8":
+            assert time.time() - t0 < 60, time.time() - t0
         rows = [ln for ln in outs[0][1].splitlines() if ln.strip() and ln.strip()[0].isdigit()]
         assert len(rows) == 2 and not any("FAIL" in ln for ln in rows), outs[0][1]
