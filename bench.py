@@ -44,7 +44,7 @@ def log(*a):
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle)
-def cpu_baseline(budget_s=12.0):
+def cpu_baseline(budget_s=18.0):
     """The host path, timed on this box's cores: AVX2 a += b over the same 1 GiB (the N=1
     workload), plus the reference's C1 config (2-rank 127.0.0.1 TCP ring, 4 MiB)."""
     import numpy as np
@@ -180,7 +180,9 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
         ok = comm.async_error() == 0 and bool((recv == float(n)).all().item())
         ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, torch.float32, M.ncclFloat, st, 1)
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
-        return {"GBps": round(count * 4 / (dt / reps) / 1e9, 2), "ok": ok}
+        i = comm.info()
+        return {"GBps": round(count * 4 / (dt / reps) / 1e9, 2), "ok": ok, "workgroups": i["channels"],
+                "pipelines": i["pipelines"], "slot_bytes": i["slot_bytes"], "scratch_MiB": i["scratch_bytes"] >> 20}
     except Exception as e:
         return {"error": str(e)[:120]}
     finally:
@@ -229,6 +231,11 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
         out["points"].append({"algo": algo, "env": {k[len("MINI_NCCL_"):].lower(): v for k, v in env.items()}, **r})
     if with_c4:  # BASELINE.json configs[3]: ring, 4 GiB fp32, SLICE x WINDOW
         out["c4_buffer_MiB"] = C4_COUNT * 4 >> 20
+        out["c4_knobs"] = ("SLICE_SIZE = payload bytes per message; WINDOW_SIZE x SIGNAL_BATCH (16) = messages in "
+                           "flight per link, the reference's bound (mini_nccl.cu:119,144,167): pipelines x 2 slots <= "
+                           "WINDOW x 16, at most 256 pipelines; scratch capped at MINI_NCCL_SCRATCH_MB (512): "
+                           "(n-1) x pipelines x 2 x SLICE <= cap, so large slices run fewer pipelines "
+                           "(csrc/schedule.h pipeline_geometry; each point reports its geometry)")
         c4 = []
         for w in C4_WINDOWS:
             for sl in C4_SLICES:
@@ -521,6 +528,13 @@ def main():
         except Exception as e:
             cpu_ring = {"error": str(e)[:200]}
 
+    if args.same_device and n > 4:
+        # rehearsal with every rank on one GPU: each rank's persistent kernel waits for the
+        # others', so all n processes' queues must be mapped at once; the GPU's scheduler maps
+        # 16 hardware queues across processes at most (8 x 2 ran at full rate, 8 x 4 -- HIP's
+        # default, which the GPU box also exports -- time-sliced ~200x slower:
+        # profiles/r2_coloc8_*); set before HIP starts.  Only this rehearsal mode does this.
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MNCCL_BENCH_SAME_DEVICE_QUEUES", "2")
     import torch
     import mini_nccl as M
     M.load()
@@ -558,19 +572,20 @@ def main():
               "data": "synthetic"}
 
     def timed(step_fn, k):
-        """K steps between barrier+sync; returns (wall s, mean per-launch event ms)."""
-        starts = [torch.cuda.Event(enable_timing=True) for _ in range(k)]
-        ends = [torch.cuda.Event(enable_timing=True) for _ in range(k)]
+        """K steps between barrier+sync; returns (wall s, mean per-launch event ms).  The two HIP
+        events bracket the K launches on the stream they run on (no event between launches: a
+        marker between back-to-back kernels costs each step ~9 us on MI355X), so the mean is
+        the launches' device time per step, inter-launch gaps included."""
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         barrier_sync()
         t0 = time.perf_counter()
+        e0.record(stream)
         for i in range(k):
-            starts[i].record(stream)
             step_fn()
-            ends[i].record(stream)
+        e1.record(stream)
         barrier_sync()
         wall = time.perf_counter() - t0
-        ev = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / k
-        return wall, ev
+        return wall, e0.elapsed_time(e1) / k
 
     if n == 1:
         g = torch.Generator(device=dev)
@@ -676,8 +691,11 @@ def main():
                                    f"HIP IPC over xGMI, {args.algo} schedule",
                        "count": count, "bytes": nbytes, "algo": args.algo, "slice_bytes": info["slice_bytes"],
                        "channels": info["channels"], "slots": info["slots"], "threads": info["threads"],
+                       "pipelines": info["pipelines"], "scratch_bytes": info["scratch_bytes"],
+                       "ranks_on_device": info["ranks_on_device"],
                        "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
-                       "auto_tune_ms": {"ring": round(info["tune_ms"][0], 4), "direct": round(info["tune_ms"][1], 4)}},
+                       "algo_rule": "MINI_NCCL_ALGO=auto: direct from 3 ranks on more than one GPU, else ring "
+                                    "(no all-reduce at init)"},
             "busbw": round(algbw * 2 * (n - 1) / n, 3),
         })
         # ceiling of each schedule from the probed links (min over ranks): ring moves
@@ -717,10 +735,10 @@ def main():
         fa = fused / (ev_ms / 1e3) / 1e9
         result["roofline"].update({"fused_alg_bytes_per_launch": fused, "fused_achieved": round(fa, 2),
                                    "fused_frac": round(fa / HBM_PEAK_GBS, 4)})
-        # the north star's "scatter-reduce sum kernel" on its own, on THIS GPU: one launch of the
-        # element-wise op over the (n-1) * chunk elements a rank reduces per call (SURVEY §8d's
-        # bytes exactly), HIP events around each launch; inside the fused kernel the same adds
-        # run at the links' pace ("The >= 70 % target")
+        # roofline.frac above is SURVEY §8(d)'s sum bytes over the FUSED all-reduce kernel's time.
+        # For reference only: the same element-wise op as a standalone launch on THIS GPU over the
+        # (n-1) * chunk elements a rank reduces per call (same bytes), HIP events around each
+        # launch -- what the sum would cost if nothing else (links, hand-offs) bounded it
         m = (n - 1) * (count // n)
         sk_ms, sk_err = 0.0, None
         # on a real node every rank has its own GPU; ranks sharing one GPU take turns
@@ -748,11 +766,12 @@ def main():
         sk_ms = max_over_ranks(sk_ms)  # every rank gets here, failed or not
         if sk_err is None and sk_ms != float("inf"):
             sk = 3 * esz * m / (sk_ms / 1e3) / 1e9
-            result["roofline"]["sum_kernel"] = {"kernel": "local_reduce_vec", "elements": m, "alg_bytes": 3 * esz * m,
-                                                "kernel_ms": round(sk_ms, 4), "achieved": round(sk, 2),
-                                                "frac": round(sk / HBM_PEAK_GBS, 4)}
+            result["roofline"]["standalone_sum_kernel_reference"] = {
+                "kernel": "local_reduce_vec (separate launch, not the all-reduce)", "elements": m,
+                "alg_bytes": 3 * esz * m, "kernel_ms": round(sk_ms, 4), "achieved": round(sk, 2),
+                "frac": round(sk / HBM_PEAK_GBS, 4)}
         else:
-            result["roofline"]["sum_kernel"] = {"error": sk_err or "failed on another rank"}
+            result["roofline"]["standalone_sum_kernel_reference"] = {"error": sk_err or "failed on another rank"}
     # the extras below (RCCL's number, the sweeps) must never cost the headline line: if they
     # have not finished in EXTRAS_LIMIT_S, every rank gives up and rank 0 prints what it has
     if n == 1 and not args.no_alt:
