@@ -134,17 +134,24 @@ def cpu_ring_baseline(n, budget_s=4.0):
 SWEEP_POINTS = [
     # (algo, knobs over the library defaults: 256 one-wave workgroups, 128 KiB slices, 2 slots,
     #  no hand-off fences, overlapped direct phases, push)
-    ("direct", {}), ("direct", {"MINI_NCCL_CHANNELS": 64, "MINI_NCCL_THREADS": 256}),
-    ("direct", {"MINI_NCCL_THREADS": 128}), ("direct", {"MINI_NCCL_CHANNELS": 512}),
-    ("direct", {"MINI_NCCL_SLOTS": 4}), ("direct", {"MINI_NCCL_SLICE_SIZE": 524288}),
-    ("direct", {"MINI_NCCL_SYS_FENCE": 1}), ("direct", {"MINI_NCCL_DIRECT_OVERLAP": 0}),
-    ("direct", {"MINI_NCCL_SLICE_SIZE": 32768}), ("direct", {"MINI_NCCL_SLICE_SIZE": 65536}),
-    ("direct", {"MINI_NCCL_CHANNELS": 128}),
-    ("ring", {}), ("ring", {"MINI_NCCL_THREADS": 128}), ("ring", {"MINI_NCCL_SLOTS": 4}),
-    ("ring", {"MINI_NCCL_SLICE_SIZE": 524288}), ("ring", {"MINI_NCCL_SYS_FENCE": 1}),
+    ("read", {}), ("read", {"MINI_NCCL_SLICE_SIZE": 32768}), ("read", {"MINI_NCCL_SLICE_SIZE": 524288}),
+    ("read", {"MINI_NCCL_CHANNELS": 128}), ("read", {"MINI_NCCL_CHANNELS": 512}),
+    ("read", {"MINI_NCCL_THREADS": 128}), ("read", {"MINI_NCCL_SYS_FENCE": 1}),
+    ("direct", {}), ("direct", {"MINI_NCCL_SLOTS": 4}), ("direct", {"MINI_NCCL_SLICE_SIZE": 524288}),
+    ("direct", {"MINI_NCCL_SLICE_SIZE": 65536}), ("direct", {"MINI_NCCL_SYS_FENCE": 1}),
+    ("ring", {}), ("ring", {"MINI_NCCL_SLOTS": 4}), ("ring", {"MINI_NCCL_SLICE_SIZE": 524288}),
     # slots in the sender's scratch, loaded over the link (pull) instead of stored into (push)
     ("direct", {"MINI_NCCL_PULL": 1}), ("ring", {"MINI_NCCL_PULL": 1}),
 ]
+ALGO_NAMES = ("ring", "direct", "read")  # mncclAlgo_t order
+
+
+def fused_bytes(algo, esz, chunk, n):
+    """Every byte one rank's fused kernel moves through its GPU's HBM per call (DESIGN.md,
+    Kernels): ring / direct read each chunk of the input and write each of the output once,
+    and 2(n-1) chunks land in and are read back from scratch: (6n - 4) chunks; read has no
+    scratch: input n, output n, plus the peers' n - 1 loads of this rank's result: 3n - 1."""
+    return esz * chunk * ((3 * n - 1) if algo == "read" else (6 * n - 4))
 C4_SLICES = [65536, 131072, 262144, 1048576]
 C4_WINDOWS = [16, 32, 64]
 # 4 GiB fp32 per rank; MNCCL_BENCH_C4_MIB / MNCCL_BENCH_C4=1 rehearse the grid smaller / at n < 8
@@ -159,7 +166,7 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
     comm = None
     try:
         comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
-        comm.set_algo(M.ALGO_DIRECT if algo == "direct" else M.ALGO_RING)
+        comm.set_algo(ALGO_NAMES.index(algo))
         st = torch.cuda.Stream(device=dev)
         send = torch.ones(count, device=dev, dtype=torch.float32)
         recv = torch.empty(count, device=dev, dtype=torch.float32)
@@ -179,8 +186,9 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
         dt = max_over_ranks(time.perf_counter() - t0)
         ok = comm.async_error() == 0 and bool((recv == float(n)).all().item())
         ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, torch.float32, M.ncclFloat, st, 1)
-        ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
         i = comm.info()
+        ok = ok and i["last_algo"] == ALGO_NAMES.index(algo)  # the point ran its own schedule
+        ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
         return {"GBps": round(count * 4 / (dt / reps) / 1e9, 2), "ok": ok, "workgroups": i["channels"],
                 "pipelines": i["pipelines"], "slot_bytes": i["slot_bytes"], "scratch_MiB": i["scratch_bytes"] >> 20}
     except Exception as e:
@@ -245,9 +253,11 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
                 r = sweep_point(M, torch, dist, dev, n, rank, env, "ring", C4_COUNT, 3, max_over_ranks)
                 c4.append({"window": w, "slice": sl, **r})
         out["c4_ring_4GiB"] = c4
-        # the same 4 GiB with the library defaults (the direct schedule from 3 ranks)
-        r = sweep_point(M, torch, dist, dev, n, rank, {}, "direct", C4_COUNT, 3, max_over_ranks)
-        out["c4_direct_4GiB_defaults"] = r
+        # the same 4 GiB with the library defaults (the read schedule) and with the direct one
+        out["c4_read_4GiB_defaults"] = sweep_point(M, torch, dist, dev, n, rank, {}, "read", C4_COUNT, 3,
+                                                   max_over_ranks)
+        out["c4_direct_4GiB_defaults"] = sweep_point(M, torch, dist, dev, n, rank, {}, "direct", C4_COUNT, 3,
+                                                     max_over_ranks)
     return out
 
 
@@ -496,8 +506,8 @@ def main():
     ap.add_argument("--count", type=int, default=0, help="elements (default: 1 GiB of --dtype)")
     ap.add_argument("--dtype", choices=["f32", "bf16", "f16"], default="f32",
                     help="f32 = the headline; bf16/f16 = BASELINE.json configs[4] (C5)")
-    ap.add_argument("--algo", choices=["auto", "ring", "direct"], default=os.environ.get("MINI_NCCL_ALGO", "auto"),
-                    help="auto = the library default (ring at 2 ranks, direct from 3: same bits, every link)")
+    ap.add_argument("--algo", choices=["auto", "ring", "direct", "read"], default=os.environ.get("MINI_NCCL_ALGO", "auto"),
+                    help="auto = the library default (read for device buffers; same bits whatever the schedule)")
     ap.add_argument("--no-alt", action="store_true", help="skip the extras: N>1 the second schedule and the RCCL reference, N=1 the host-inclusive rate")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true", help="N>1: skip the configuration sweeps")
@@ -592,8 +602,9 @@ def main():
         g.manual_seed(1234)
         a = torch.rand(count, device=dev, generator=g, dtype=torch.float32).to(tdt)
         b = torch.rand(count, device=dev, generator=g, dtype=torch.float32).to(tdt)
-        # parity spot check of one step against torch fp32 (the op is one IEEE add: bit-exact)
-        ref = (a[: 1 << 20] + b[: 1 << 20]).clone()
+        # parity: every step is one IEEE add per element (bf16/f16: correctly rounded), so torch's
+        # own add over the FULL buffer, repeated as many times, must give the same bits
+        a0 = a.clone()
         sh = stream.cuda_stream
 
         def step():
@@ -603,10 +614,17 @@ def main():
 
         step()
         torch.cuda.synchronize()
-        exact = bool(torch.equal(a[: 1 << 20], ref))  # one IEEE add (bf16/f16: correctly rounded) per element
+        ref = a0 + b
+        exact = bool(torch.equal(a, ref))  # first step, all `count` elements
         for _ in range(args.warmup):
             step()
         wall, ev_ms = timed(step, args.steps)
+        # every step of the job (1 + warmup + timed), recomputed by torch, compared bit for bit
+        for _ in range(args.warmup + args.steps):
+            ref.add_(b)
+        torch.cuda.synchronize()
+        exact_all = bool(torch.equal(a, ref))
+        del ref, a0
         ms = wall / args.steps * 1e3
         alg_bytes = 3 * nbytes
         result.update({
@@ -614,7 +632,8 @@ def main():
             "ms_per_step": round(ms, 4),
             "config": {"workload": f"1-GPU local reduce a <- a + b, 1 GiB {args.dtype} (BASELINE.md row '1-GPU local reduce')",
                        "count": count, "bytes": nbytes, "kernel": f"local_reduce_vec<{args.dtype},Sum>",
-                       "parity_step_exact": exact},
+                       "parity_step_exact": exact, "parity_all_steps_exact": exact_all,
+                       "parity_check": "full buffer vs torch's own add repeated 1 + warmup + steps times"},
         })
         traffic, tsrc = pmc_traffic(f"local_reduce_{args.dtype}_1GiB")
         kern_key = "local_reduce_vec"
@@ -622,7 +641,7 @@ def main():
         comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
         info = comm.info()
         if args.algo == "auto":
-            args.algo = "direct" if info["algo"] == M.ALGO_DIRECT else "ring"
+            args.algo = ALGO_NAMES[info["algo"]]
         send = torch.ones(count, device=dev, dtype=tdt)
         recv = torch.empty(count, device=dev, dtype=tdt)
         sh = stream.cuda_stream
@@ -635,7 +654,7 @@ def main():
             return step
 
         def run_algo(algo):
-            comm.set_algo(M.ALGO_DIRECT if algo == "direct" else M.ALGO_RING)
+            comm.set_algo(ALGO_NAMES.index(algo))
             step = make_step()
             recv.fill_(-1.0)
             for _ in range(max(1, args.warmup)):
@@ -647,6 +666,7 @@ def main():
             ok = ok and ae == 0 and bool((recv == float(n)).all().item())
             # then 3 calls on varying data (outside the timed region), restoring the buffers
             ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream)
+            ok = ok and comm.info()["last_algo"] == ALGO_NAMES.index(algo)  # no fallback happened
             send.fill_(1.0)
             ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
             return max_over_ranks(wall), max_over_ranks(ev_ms), ok
@@ -694,31 +714,43 @@ def main():
                        "pipelines": info["pipelines"], "scratch_bytes": info["scratch_bytes"],
                        "ranks_on_device": info["ranks_on_device"],
                        "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
-                       "algo_rule": "MINI_NCCL_ALGO=auto: direct from 3 ranks on more than one GPU, else ring "
-                                    "(no all-reduce at init)"},
+                       "algo_rule": "MINI_NCCL_ALGO=auto: read (peers' buffers loaded over the links, no scratch) "
+                                    "for device buffers; otherwise direct from 3 ranks on more than one GPU, else "
+                                    "ring (no all-reduce at init)"},
             "busbw": round(algbw * 2 * (n - 1) / n, 3),
         })
         # ceiling of each schedule from the probed links (min over ranks): ring moves
         # 2(n-1)/n of the buffer through one link, direct 2/n through each of n-1 links
+        # read moves the same 2/n through each link as direct, as loads (the probe's mesh pull)
         if "probe_next_GBps" in link:
             ring_ceiling = link["probe_next_GBps"] * n / (2 * (n - 1))
             direct_ceiling = link["probe_mesh_GBps_per_link"] * n / 2
+            link.update({"ring_ceiling_GBps": round(ring_ceiling, 2), "direct_ceiling_GBps": round(direct_ceiling, 2)})
             ceiling = direct_ceiling if args.algo == "direct" else ring_ceiling
-            link.update({"ring_ceiling_GBps": round(ring_ceiling, 2), "direct_ceiling_GBps": round(direct_ceiling, 2),
-                         "frac": round(algbw / ceiling, 4)})
+            pull = link.get("probe_variants_GBps_per_link", {}).get("mesh_pull_sys")
+            if pull:
+                link["read_ceiling_GBps"] = round(pull * n / 2, 2)
+                if args.algo == "read":
+                    ceiling = pull * n / 2
+            link["frac"] = round(algbw / ceiling, 4)
         result["link"] = link
         if rank == 0:
             arm(result)
         if not args.no_alt:
-            other = "direct" if args.algo == "ring" else "ring"
-            try:
-                w2, e2, ok2 = run_algo(other)
-                ms2 = w2 / args.steps * 1e3
-                result["alt"] = {"algo": other, "value": round(nbytes / (ms2 / 1e3) / 1e9, 3), "ms_per_step": round(ms2, 4),
-                                 "kernel_ms": round(e2, 4), "result_check": "ok" if ok2 else "FAILED"}
-            except Exception as e:
-                result["alt"] = {"algo": other, "error": str(e)}
-            comm.set_algo(M.ALGO_DIRECT if args.algo == "direct" else M.ALGO_RING)
+            # the other schedules on the same buffers (same bits), for comparison
+            result["alt"] = []
+            for other in (a for a in ALGO_NAMES if a != args.algo):
+                try:
+                    w2, e2, ok2 = run_algo(other)
+                    ms2 = w2 / args.steps * 1e3
+                    result["alt"].append({"algo": other, "value": round(nbytes / (ms2 / 1e3) / 1e9, 3),
+                                          "ms_per_step": round(ms2, 4), "kernel_ms": round(e2, 4),
+                                          "result_check": "ok" if ok2 else "FAILED"})
+                except Exception as e:
+                    result["alt"].append({"algo": other, "error": str(e)[:200]})
+                if rank == 0:
+                    arm(result)
+            comm.set_algo(ALGO_NAMES.index(args.algo))
         traffic, tsrc = pmc_traffic(f"{args.algo}_{args.dtype}_1GiB_n{n}")
         kern_key = f"{args.algo}_kernel"
     achieved = alg_bytes / (ev_ms / 1e3) / 1e9
@@ -729,9 +761,8 @@ def main():
         result["roofline"]["traffic_source"] = tsrc
     if n > 1:
         # `achieved` counts SURVEY.md §8(d)'s sum-kernel bytes only; the fused kernel also does
-        # the raw send and the all-gather: every byte one rank reads or writes, local or pushed
-        # to a peer, is esz * chunk * (6n - 4) for both schedules (Kernels)
-        fused = esz * (count // n) * (6 * n - 4)
+        # the raw send and the all-gather (fused_bytes: every byte through this rank's HBM)
+        fused = fused_bytes(args.algo, esz, count // n, n)
         fa = fused / (ev_ms / 1e3) / 1e9
         result["roofline"].update({"fused_alg_bytes_per_launch": fused, "fused_achieved": round(fa, 2),
                                    "fused_frac": round(fa / HBM_PEAK_GBS, 4)})

@@ -24,13 +24,19 @@
 extern "C" {
 #endif
 
-/* schedules; both produce bit-identical results (same fold order per element) */
+/* schedules; all produce bit-identical results (same fold order per element) */
 typedef enum {
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
-  mncclAlgoDirect = 1  /* every peer pushes its slice of chunk c straight to rank c over its
+  mncclAlgoDirect = 1, /* every peer pushes its slice of chunk c straight to rank c over its
                           own xGMI link; c folds them in ring order c, c+1, ..., c-1 and
                           pushes the result to every peer (MINI_NCCL_ALGO=auto: from 3 ranks
                           on, when the ranks are on more than one GPU) */
+  mncclAlgoRead = 2    /* no scratch: rank c loads the peers' slices of chunk c straight from
+                          their send buffers (mapped per allocation, negotiated per call),
+                          folds them in the same order into its recv, and every peer loads
+                          the result from there; a call whose buffers some rank cannot share
+                          (host memory, graph capture) runs the scratch schedule instead, on
+                          every rank alike */
 } mncclAlgo_t;
 
 typedef struct {
@@ -53,6 +59,12 @@ typedef struct {
   int ranks_on_device;    /* ranks of this communicator on this rank's GPU (itself included) */
   size_t slot_bytes;      /* largest payload per message (MINI_NCCL_SLICE_SIZE unless the
                              scratch cap MINI_NCCL_SCRATCH_MB shrank it) */
+  int last_algo;          /* schedule the last all-reduce ran (mncclAlgo_t; -1: no kernel
+                             yet): mncclAlgoRead falls back to the scratch schedule for a
+                             call some rank's buffers cannot take part in */
+  size_t peer_mappings;   /* read schedule: peer allocations mapped into this process */
+  int scratch_algo;       /* the read schedule's fallback (ring or direct), chosen from the
+                             ranks' GPUs: direct from 3 ranks on more than one GPU */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,

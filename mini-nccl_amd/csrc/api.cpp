@@ -160,6 +160,9 @@ ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info) {
   info->pipelines = c->wave_channels();
   info->ranks_on_device = c->ranks_on_device();
   info->slot_bytes = c->wave_slice();
+  info->last_algo = c->last_algo();
+  info->peer_mappings = c->peer_mappings();
+  info->scratch_algo = c->scratch_algo();
   return ncclSuccess;
 }
 
@@ -167,7 +170,7 @@ ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info) {
 // schedules' messages share mailboxes and slots), as with any other communicator setting.
 ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo) {
   if (!comm) return ncclInvalidArgument;
-  if (algo != mncclAlgoRing && algo != mncclAlgoDirect) return ncclInvalidArgument;
+  if (algo != mncclAlgoRing && algo != mncclAlgoDirect && algo != mncclAlgoRead) return ncclInvalidArgument;
   reinterpret_cast<Comm*>(comm)->set_algo(algo);
   return ncclSuccess;
 }

@@ -109,9 +109,11 @@ constexpr uint32_t kInfoMagic = 0x4d4e4932u;  // 'MNI2'
 
 Comm::Comm(int nranks, int rank, const std::string& ip) : rank_(rank), nranks_(nranks) {
   cfg_ = Config::from_env();
-  // auto: the reference's ring; from 3 ranks on GPUs of their own, the direct schedule (same
-  // bits, every xGMI link of the mesh) -- decided from the peers' devices in exchange_and_map
-  algo_ = cfg_.algo >= 0 ? cfg_.algo : 0;
+  // auto: the read schedule (same bits; no scratch; each call falls back to a scratch schedule
+  // when some rank's buffers cannot be shared) -- the scratch schedule is decided from the
+  // peers' devices in exchange_and_map
+  algo_ = cfg_.algo >= 0 ? cfg_.algo : 2;
+  scratch_algo_ = cfg_.algo == 1 ? 1 : 0;
   if (nranks > kMaxRanks) throw std::invalid_argument("nRanks > 16 is not supported on one node");
   geo_ = pipeline_geometry(nranks, cfg_.channels, cfg_.threads, cfg_.window_size, cfg_.signal_batch, cfg_.slots,
                            cfg_.slice_size, cfg_.scratch_cap);
@@ -213,18 +215,20 @@ void Comm::exchange_and_map() {
           "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SIGNAL_BATCH / SLOTS / CHANNELS / THREADS / SCRATCH_MB / MIN_SLICE / "
           "PIPE_DEPTH / DIRECT_OVERLAP / PULL / ALGO / TUNE / TUNE_BYTES differ between ranks");
   }
-  // the schedule for MINI_NCCL_ALGO=auto, the same on every rank (computed from the gathered
-  // records): from 3 ranks, `direct` when the ranks are on more than one GPU (each pair of an
-  // MI355X node has its own xGMI link; direct uses all of them, the ring one); `ring` when every
-  // rank shares one GPU (no links: the ring's neighbour-only coupling measured faster there,
-  // profiles/r2_direct_sweep_n4_same_gpu.txt) and at 2 ranks (one link either way)
+  // the scratch schedule of MINI_NCCL_ALGO=auto / read (the read schedule's fallback), the same
+  // on every rank (computed from the gathered records): from 3 ranks, `direct` when the ranks are
+  // on more than one GPU (each pair of an MI355X node has its own xGMI link; direct uses all of
+  // them, the ring one); `ring` when every rank shares one GPU (no links: the ring's
+  // neighbour-only coupling measured faster there, profiles/r2_direct_sweep_n4_same_gpu.txt)
+  // and at 2 ranks (one link either way)
   bool one_device = true;
   ranks_on_device_ = 0;
   for (int q = 0; q < nranks_; ++q) {
     if (all[(size_t)q].pci != all[0].pci) one_device = false;
     if (all[(size_t)q].pci == me.pci) ++ranks_on_device_;
   }
-  if (cfg_.algo < 0) algo_ = (nranks_ >= 3 && !one_device) ? 1 : 0;
+  const int rule = (nranks_ >= 3 && !one_device) ? 1 : 0;
+  if (cfg_.algo < 0 || cfg_.algo == 2) scratch_algo_ = rule;
   // Rank PROCESSES sharing this GPU: a persistent kernel waits for its peers' kernels, so all of
   // them must be resident at once; the GPU's scheduler maps a bounded number of processes and
   // hardware queues together, beyond which it time-slices and every hand-off waits for a turn
@@ -277,6 +281,11 @@ void Comm::exchange_and_map() {
   }
   // every rank has mapped every peer and its own memory is zeroed before anyone writes
   boot_.barrier();
+  // the read schedule's per-call board (collective; unavailable on every rank alike if shared
+  // memory is)
+  std::vector<uint64_t> nonces((size_t)nranks_);
+  for (int q = 0; q < nranks_; ++q) nonces[(size_t)q] = all[(size_t)q].nonce;
+  pbuf_.init(boot_, rank_, nranks_, nonces, cfg_.port);
 }
 
 // MINI_NCCL_ALGO=auto with MINI_NCCL_TUNE=1 (opt-in; the default decides from the devices, see
@@ -347,6 +356,7 @@ Comm::~Comm() {
         peer_opened_[(size_t)q] = false;
       }
     }
+    pbuf_.close_all();
     try {
       if (sticky_ == ncclSuccess) boot_.barrier();  // nobody still maps my memory
     } catch (...) {
@@ -356,6 +366,7 @@ Comm::~Comm() {
 }
 
 void Comm::release() {
+  pbuf_.close_all();
   for (int q = 0; q < (int)peer_opened_.size(); ++q) {
     if (peer_opened_[(size_t)q]) {
       hipIpcCloseMemHandle(peer_scratch_[(size_t)q]);
@@ -489,8 +500,18 @@ void Comm::wait_previous_call() {
   if (have_last_) hip_check(hipEventSynchronize(order_ev_), "wait for the previous call");
 }
 
-void Comm::launch_ring_or_direct(const void* send, void* recv, size_t chunk_bytes, int dtype, int op,
-                                 hipStream_t stream, uint32_t seq) {
+bool Comm::device_local(const void* p) const {
+  hipPointerAttribute_t a;
+  memset(&a, 0, sizeof a);
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice && !a.isManaged && a.device == device_;
+}
+
+void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
+                  uint32_t seq, bool vec, const char* const* psend, const char* const* precv) {
   const int n = nranks_;
   CollParams p;
   memset(&p, 0, sizeof p);
@@ -512,6 +533,8 @@ void Comm::launch_ring_or_direct(const void* send, void* recv, size_t chunk_byte
   for (int q = 0; q < n; ++q) {
     p.peer_scratch[q] = peer_scratch_[(size_t)q];
     p.peer_mbox[q] = peer_mbox_[(size_t)q];
+    if (psend) p.peer_send[q] = psend[q];
+    if (precv) p.peer_recv[q] = precv[q];
   }
   p.status = d_ctl_;
   p.host_abort = d_ctl_ + 1;
@@ -521,13 +544,12 @@ void Comm::launch_ring_or_direct(const void* send, void* recv, size_t chunk_byte
   p.sys_fence = cfg_.sys_fence;
   p.direct_overlap = cfg_.direct_overlap;
   p.pull = cfg_.pull;
-  // 16-byte vector path whenever every message's local base is dword-aligned (vectors may
-  // straddle 16-byte boundaries on the local side; each message's last len % 16 bytes go
-  // element by element); element-wise path otherwise (2-byte types with odd chunks)
-  const bool vec = (((uintptr_t)send | (uintptr_t)recv) % 4 == 0) && (chunk_bytes % 4 == 0);
-  hipError_t e = algo_ == 1 ? launch_direct(dtype, op, vec, geo_.workgroups, cfg_.threads, p, stream)
-                            : launch_ring(dtype, op, vec, geo_.workgroups, cfg_.threads, p, stream);
+  const int nt = cfg_.threads, wg = geo_.workgroups;
+  hipError_t e = algo == 2   ? launch_read(dtype, op, vec, wg, nt, p, stream)
+                 : algo == 1 ? launch_direct(dtype, op, vec, wg, nt, p, stream)
+                             : launch_ring(dtype, op, vec, wg, nt, p, stream);
   hip_check(e, "kernel launch");
+  last_algo_ = algo;
 }
 
 ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t stream) {
@@ -596,9 +618,43 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
       hip_check(hipMemcpyAsync((char*)krecv + body, (const char*)ksend + body, bytes - body, hipMemcpyDefault,
                                stream),
                 "tail copy");
+    // 16-byte vector path whenever every message's local base is dword-aligned (vectors may
+    // straddle 16-byte boundaries on the local side; each message's last len % 16 bytes go
+    // element by element); element-wise path otherwise (2-byte types with odd chunks)
+    bool vec = (((uintptr_t)ksend | (uintptr_t)krecv) % 4 == 0) && (chunk_bytes % 4 == 0);
+    int algo = algo_ == 2 ? scratch_algo_ : algo_;
+    const char* psend[kMaxRanks] = {};
+    const char* precv[kMaxRanks] = {};
+    if (algo_ == 2 && pbuf_.available()) {
+      // the read schedule: every rank takes part in the rendezvous, all decide alike
+      const bool eligible = !capturing && ksend == send && krecv == recv && device_local(send) && device_local(recv);
+      bool vec_all = false;
+      PeerBuffers::Decision d = PeerBuffers::kFallback;
+      try {
+        // a peer that does not reach the call within the watchdog's limit fails it, as the
+        // kernel's own wait would (the reference's 10 s watchdog, mini_nccl.cu:200-214)
+        d = pbuf_.negotiate(send, recv, eligible, count, dtype, op, cfg_.timeout_ms / 1000.0 + 2.0,
+                            [this] { wait_previous_call(); }, psend, precv, &vec_all);
+      } catch (const std::exception& e) {
+        fprintf(stderr, "[Mini-NCCL] rank %d: %s; communicator is no longer usable\n", rank_, e.what());
+        sticky_ = ncclInternalError;
+        if (cur_dev != device_) hipSetDevice(cur_dev);
+        return sticky_;
+      }
+      if (d == PeerBuffers::kMismatch) {
+        fprintf(stderr, "[Mini-NCCL] rank %d: ranks called ncclAllReduce with different count / datatype / op\n",
+                rank_);
+        if (cur_dev != device_) hipSetDevice(cur_dev);
+        return ncclInvalidUsage;
+      }
+      if (d == PeerBuffers::kRead) {
+        algo = 2;
+        vec = vec_all && (chunk_bytes % 4 == 0);
+      }
+    }
     seq = ++call_seq_;
     if (seq == 0) seq = ++call_seq_;  // 0 = "no kernel" (wait_for)
-    launch_ring_or_direct(ksend, krecv, chunk_bytes, dtype, op, stream, seq);
+    launch(algo, ksend, krecv, chunk_bytes, dtype, op, stream, seq, vec, psend, precv);
     if (rr == Reach::kStaged) hip_check(hipMemcpyAsync(recv, stage_, bytes, hipMemcpyDefault, stream), "stage out");
   }
   if (!capturing) {

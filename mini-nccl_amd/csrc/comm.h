@@ -12,6 +12,7 @@
 #include "config.h"
 #include "kernels.h"
 #include "mini_nccl_api.h"
+#include "peerbuf.h"
 #include "schedule.h"
 
 namespace mnccl {
@@ -33,6 +34,9 @@ class Comm {
   const Config& config() const { return cfg_; }
   int algo() const { return algo_; }
   void set_algo(int a) { algo_ = a; }
+  int last_algo() const { return last_algo_; }  // schedule of the last launched kernel, -1: none
+  size_t peer_mappings() const { return pbuf_.mapped_allocations(); }
+  int scratch_algo() const { return scratch_algo_; }
   // calibration of MINI_NCCL_ALGO=auto with MINI_NCCL_TUNE=1 (max over ranks, ms per call; 0 = not run)
   double tune_ms(int a) const { return tune_ms_[a & 1]; }
   // rank processes / communicators whose GPU is this rank's GPU (this rank included)
@@ -58,15 +62,19 @@ class Comm {
   enum class Reach { kDevice, kMapped, kStaged };
   Reach reach(const void* p, const void** kernel_ptr) const;
   void ensure_stage(size_t bytes, hipStream_t stream);
-  void launch_ring_or_direct(const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
-                             uint32_t seq);
+  // algo: 0 ring, 1 direct, 2 read (psend / precv: every rank's buffers mapped here)
+  void launch(int algo, const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
+              uint32_t seq, bool vec, const char* const* psend = nullptr, const char* const* precv = nullptr);
+  bool device_local(const void* p) const;  // device memory of this rank's GPU (not managed)
   void wait_previous_call();
   ncclResult_t check_status();
 
   int rank_, nranks_, device_ = 0;
   Config cfg_;
   Geometry geo_;
-  int algo_ = 0;
+  int algo_ = 0;                 // 0 ring, 1 direct, 2 read
+  int last_algo_ = -1;
+  int scratch_algo_ = 0;         // ring or direct: the read schedule's fallback (and auto's rule)
   int ranks_on_device_ = 1;
   uint32_t call_seq_ = 0;        // kernel launches of this communicator (the kernel's start word)
   double tune_ms_[2] = {0.0, 0.0};
@@ -83,6 +91,7 @@ class Comm {
   std::vector<char*> peer_scratch_;
   std::vector<uint64_t*> peer_mbox_;
   std::vector<bool> peer_opened_;  // true: mapped with hipIpcOpenMemHandle (close on destroy)
+  PeerBuffers pbuf_;               // read schedule: per-call rendezvous + peers' buffer mappings
 
   char* stage_ = nullptr;         // device staging copy for pageable host buffers (grown on demand)
   size_t stage_bytes_ = 0;

@@ -59,8 +59,9 @@ Config Config::from_env() {
   if (a && *a) {
     if (!strcmp(a, "ring")) c.algo = 0;
     else if (!strcmp(a, "direct")) c.algo = 1;
+    else if (!strcmp(a, "read")) c.algo = 2;
     else if (!strcmp(a, "auto")) c.algo = -1;
-    else throw std::invalid_argument(std::string("MINI_NCCL_ALGO=") + a + " (expected auto|ring|direct)");
+    else throw std::invalid_argument(std::string("MINI_NCCL_ALGO=") + a + " (expected auto|ring|direct|read)");
   }
   c.blocking = env_int("MINI_NCCL_BLOCKING", 1) != 0;
   c.sys_fence = env_int("MINI_NCCL_SYS_FENCE", 0) != 0;
@@ -90,7 +91,7 @@ std::string Config::describe() const {
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, scratch_cap=%zu MiB, algo=%s, "
            "blocking=%d, sys_fence=%d, min_slice=%zu, depth=%d, pull=%d, tune=%d, stage_host=%d, timeout=%.0f ms, port=%d",
            slice_size, window_size, signal_batch, slots, channels, threads, scratch_cap >> 20,
-           algo < 0 ? "auto" : algo ? "direct" : "ring", blocking,
+           algo < 0 ? "auto" : algo == 2 ? "read" : algo ? "direct" : "ring", blocking,
            sys_fence, min_slice, pipe_depth, pull, tune, stage_host, timeout_ms, port);
   return b;
 }

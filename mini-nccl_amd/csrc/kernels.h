@@ -33,6 +33,8 @@ struct CollParams {
   int32_t sys_fence;       // system-scope release fence before each ready flag
   int32_t direct_overlap;  // direct: next iteration's raw pushes before this one's results
   int32_t pull;            // slots in the sender's scratch, loaded over the link (schedule.h)
+  const char* peer_send[16];  // read schedule: every rank's send buffer, mapped here (own at [rank])
+  const char* peer_recv[16];  // read schedule: every rank's recv buffer, mapped here
 };
 
 constexpr int kMaxRanks = 16;
@@ -43,6 +45,8 @@ hipError_t launch_ring(int dtype, int op, bool vec, int channels, int threads,
                        const CollParams& p, hipStream_t stream);
 hipError_t launch_direct(int dtype, int op, bool vec, int channels, int threads,
                          const CollParams& p, hipStream_t stream);
+hipError_t launch_read(int dtype, int op, bool vec, int channels, int threads,
+                       const CollParams& p, hipStream_t stream);
 // out[i] = op(local[i], incoming[i]) for i < count
 hipError_t launch_local_reduce(int dtype, int op, void* out, const void* local,
                                const void* incoming, uint64_t count, hipStream_t stream);

@@ -628,6 +628,156 @@ aborted:
     for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), 1ull);
 }
 
+// ---------------------------------------------------------------- read kernel
+// MINI_NCCL_ALGO=read (schedule.h): no scratch.  Comm maps every peer's send and recv buffers
+// (HIP IPC, negotiated per call); rank r folds slice s of its own chunk r straight from the
+// peers' send buffers (sc0 sc1 loads over the links, the direct schedule's fold order), stores
+// the result into its own recv with sc0 sc1 (write-through: the peers' loads see it once the
+// wave drained), raises READY, and copies every peer's result slice out of that peer's recv.
+//
+// Fold of slice `nbytes` at byte `coff` of chunk r: acc = op(x_q, acc) in ring order.
+template <typename T, int OPC>
+__device__ __forceinline__ void read_fold_scalar(const CollParams& p, uint64_t coff, uint32_t nbytes, int lane,
+                                                 uint32_t off0) {
+  const int n = p.n, r = p.rank;
+  typedef typename Scal<sizeof(T)>::U Us;
+  const rsrc_t out = make_rsrc(p.recv + coff, nbytes);
+  const uint32_t ne = nbytes / sizeof(T);
+  for (uint32_t i = off0 / sizeof(T) + lane; i < ne; i += 64) {
+    T acc = reinterpret_cast<const T*>(p.send + coff)[i];
+    for (int k = 1; k < n; ++k) {
+      const rsrc_t in = make_rsrc(p.peer_send[direct_peer(n, r, k)] + coff, nbytes);
+      acc = Op<T, OPC>::f(__builtin_bit_cast(T, Scal<sizeof(T)>::ld(in, i * (uint32_t)sizeof(T))), acc);
+    }
+    Scal<sizeof(T)>::st(out, i * (uint32_t)sizeof(T), __builtin_bit_cast(Us, acc));
+  }
+}
+
+template <typename T, int OPC, bool VEC>
+__device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, uint32_t nbytes, int lane) {
+  if (!VEC) {
+    read_fold_scalar<T, OPC>(p, coff, nbytes, lane, 0);
+    return;
+  }
+  const int n = p.n, r = p.rank;
+  constexpr int U = kFoldU;
+  const rsrc_t out = make_rsrc(p.recv + coff, nbytes);
+  const char* lsrc = p.send + coff;
+  const uint32_t nvec = nbytes >> 4;
+  uint32_t b = 0;
+  // full batches: the n-1 remote streams are issued back to back (one peer ahead of the fold)
+  for (; b + 64 * U <= nvec; b += 64 * U) {
+    v4u acc[U], cur[U], nxt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = ld_g16(lsrc + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16);
+    {
+      const rsrc_t in = make_rsrc(p.peer_send[direct_peer(n, r, 1)] + coff, nbytes);
+#pragma unroll
+      for (int u = 0; u < U; ++u) cur[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
+    }
+    for (int k = 1; k < n; ++k) {
+      if (k + 1 < n) {
+        const rsrc_t in = make_rsrc(p.peer_send[direct_peer(n, r, k + 1)] + coff, nbytes);
+#pragma unroll
+        for (int u = 0; u < U; ++u) nxt[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] = reduce16<T, OPC>(cur[u], acc[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
+  }
+  for (uint32_t i = b + (uint32_t)lane; i < nvec; i += 64) {
+    v4u acc = ld_g16(lsrc + (size_t)i * 16);
+    for (int k = 1; k < n; ++k) {
+      const rsrc_t in = make_rsrc(p.peer_send[direct_peer(n, r, k)] + coff, nbytes);
+      acc = reduce16<T, OPC>(ld_slot16(in, i * 16), acc);
+    }
+    st_slot16(out, i * 16, acc);
+  }
+  if (nbytes & 15u) read_fold_scalar<T, OPC>(p, coff, nbytes, lane, nvec * 16);
+}
+
+// Messages per (pair, pipeline) and call: START (my send is readable: the call began on my
+// stream), READY(t) for t < iters (my result slice of iteration t is in my recv), DONE (I no
+// longer read your buffers: your stream may go on).  Order per pipeline: START, F0, F1, G0, F2,
+// G1, ..., G(I-1), DONE -- the next fold's loads leave before this iteration's results are
+// awaited.  DONE also returns credits for every message (the scratch schedules' slot counters
+// continue across calls, whatever the schedule).
+template <typename T, int OPC, bool VEC>
+__global__ void __launch_bounds__(kMaxThreads) read_kernel(CollParams p) {
+  signal_start(p);
+  const WaveId id = wave_id();
+  const int lane = id.lane, w = id.w, C = id.C, wv = id.wv;
+  const int n = p.n, r = p.rank;
+  __shared__ u64 s_tx[kMaxWaves][kMaxRanks], s_rx[kMaxWaves][kMaxRanks];
+  u64* tx = s_tx[wv];
+  u64* rx = s_rx[wv];
+  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox};
+  const uint32_t iters = p.iters;
+  const u64 mpc = read_msgs_per_call(iters);
+  if (lane < n) {
+    tx[lane] = p.tx_seq[(u64)lane * C + w];
+    rx[lane] = p.rx_seq[(u64)lane * C + w];
+  }
+  __builtin_amdgcn_wave_barrier();
+  // START to every peer, then wait for theirs
+  if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + 1);
+  for (int k = 1; k < n; ++k) {
+    const int q = direct_peer(n, r, k);
+    if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx[q] + 1, ctl, lane)) goto aborted;
+  }
+  acquire_sys(p.sys_fence);
+  for (uint32_t j = 0; j <= iters; ++j) {
+    if (j < iters) {
+      // F(j): fold my chunk's slice j from the peers' send buffers, store, drain, READY
+      const u64 s = (u64)j * C + w;
+      const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
+      if (len) read_fold<T, OPC, VEC>(p, (u64)r * p.chunk_bytes + s * p.slice_bytes, len, lane);
+      drain_stores();
+      if (p.sys_fence && lane == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + 2 + j);
+    }
+    if (j > 0) {
+      // G(j-1): every peer's result slice j-1, peer by peer (pipeline w starts at peer w mod
+      // n-1, so a rank's pipelines spread over all links), into my recv
+      const uint32_t t = j - 1;
+      const u64 s = (u64)t * C + w;
+      const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
+      for (int k = 1; k < n; ++k) {
+        const int q = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));
+        if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx[q] + 2 + t, ctl, lane)) goto aborted;
+        acquire_sys(p.sys_fence);
+        if (len) {
+          const u64 coff = (u64)q * p.chunk_bytes + s * p.slice_bytes;
+          const rsrc_t in = make_rsrc(p.peer_recv[q] + coff, len);
+          move<T, OPC, VEC, kCopy, kPushU>(nullptr, p.recv + coff, in, in, len, lane);
+        }
+      }
+    }
+  }
+  // DONE: every load of a peer's buffer has returned; then wait until nobody reads mine
+  drain_stores();
+  if (lane < n && lane != r) {
+    st_sys(p.peer_mbox[lane] + mbox_credit(n, C, r, w), rx[lane] + mpc);
+    st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + mpc);
+  }
+  for (int k = 1; k < n; ++k) {
+    const int q = direct_peer(n, r, k);
+    if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx[q] + mpc, ctl, lane)) goto aborted;
+  }
+  if (lane < n && lane != r) {
+    p.tx_seq[(u64)lane * C + w] = tx[lane] + mpc;
+    p.rx_seq[(u64)lane * C + w] = rx[lane] + mpc;
+  }
+  return;
+aborted:
+  if (lane == 0)
+    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), 1ull);
+}
+
 // ---------------------------------------------------------------- local reduce
 // One 16-byte vector per lane, one wave per workgroup, one workgroup per 1 KiB of output,
 // non-temporal loads and stores (the bytes are touched once).  Measured on MI355X for
@@ -780,6 +930,21 @@ static hipError_t direct_for_t(int op, bool vec, int C, int nt, const CollParams
 }
 
 template <typename T>
+static hipError_t read_for_t(int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
+#define READ_CASE(OPC)                                                                           \
+  case OPC:                                                                                      \
+    if (vec) hipLaunchKernelGGL((read_kernel<T, OPC, true>), dim3(C), dim3(nt), 0, st, p);      \
+    else hipLaunchKernelGGL((read_kernel<T, OPC, false>), dim3(C), dim3(nt), 0, st, p);         \
+    break;
+  switch (op) {
+    READ_CASE(kSum) READ_CASE(kProd) READ_CASE(kMax) READ_CASE(kMin)
+    default: return hipErrorInvalidValue;
+  }
+#undef READ_CASE
+  return hipGetLastError();
+}
+
+template <typename T>
 static hipError_t local_for_t(int op, void* out, const void* a, const void* b, u64 count, hipStream_t st) {
   // 16-byte vectors over the body whenever the three buffers are dword-aligned (4-byte-aligned
   // dwordx4 accesses are valid on gfx950), then the last (bytes % 16) bytes element-wise
@@ -816,6 +981,12 @@ hipError_t launch_ring(int dtype, int op, bool vec, int C, int nt, const CollPar
 
 hipError_t launch_direct(int dtype, int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
 #define M(T) return direct_for_t<T>(op, vec, C, nt, p, st)
+  MNCCL_DISPATCH_T(dtype, M)
+#undef M
+}
+
+hipError_t launch_read(int dtype, int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
+#define M(T) return read_for_t<T>(op, vec, C, nt, p, st)
   MNCCL_DISPATCH_T(dtype, M)
 #undef M
 }

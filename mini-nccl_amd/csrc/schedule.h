@@ -85,6 +85,12 @@ MNCCL_HD RingOp ring_op(int n, int r, int k) {
 MNCCL_HD int direct_peer(int n, int r, int k) { return mod_n(r + k, n); }  // k = 1..n-1
 MNCCL_HD int direct_msgs_per_iter() { return 2; }  // per (pair, channel): raw, then final
 
+// Read schedule (MINI_NCCL_ALGO=read): no scratch; the same fold as direct, but rank r loads
+// the peers' raw slices of chunk r straight from their send buffers and each peer's result
+// slice from that peer's recv (Comm maps the peers' buffers).  Messages per (pair, pipeline)
+// and call, all on the READY word: START, one per iteration (result slice ready), DONE.
+MNCCL_HD uint64_t read_msgs_per_call(uint32_t iters) { return (uint64_t)iters + 2; }
+
 // Direct phases of one pipeline, in execution order: A(t) pushes raw slices of iteration t,
 // B(t) folds and pushes results, C(t) copies the arriving results.  Plain order A0 B0 C0 A1 B1
 // C1 ...; overlapped order A0 B0 A1 C0 B1 A2 C1 ... B(I-1) C(I-1): the next iteration's raw

@@ -117,8 +117,10 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
                 detail = (f"got {got[first]!r} expected {exp[first]!r}" if bad and first >= 0 else "")
             elif rc != 0:
                 bad, first = -1, -1
+            ci = comm.info()
             results.append({"case": case, "rc": rc, "bad": bad, "first": first, "detail": detail, "secs": dt,
-                            "async": comm.async_error()})
+                            "async": comm.async_error(), "last_algo": ci["last_algo"],
+                            "peer_mappings": ci["peer_mappings"]})
             send.free()
             if not inplace:
                 recv.free()
@@ -260,6 +262,38 @@ def init_rank(rank, n, port, env, out_q):
         if rc == 0:
             M.load().ncclCommDestroy(h)
         out_q.put((rank, {"rc": rc}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
+def mismatch_rank(rank, n, port, env, out_q):
+    """Read schedule: ranks pass different counts to one call (a caller bug the reference would
+    hang or corrupt on) -> every rank gets ncclInvalidUsage from the per-call rendezvous, and the
+    communicator stays usable: a matching call right after is bit-exact."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        hip_rt.set_device(0)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        st = hip_rt.Stream()
+        count = 40000
+        xs = O.random_inputs(n, count, "f32", seed=321)
+        send, recv = hip_rt.DeviceBuffer(count * 4), hip_rt.DeviceBuffer(count * 4)
+        send.upload(xs[rank])
+        rc_bad = comm.all_reduce(send.ptr, recv.ptr, count - rank, M.ncclFloat, M.ncclSum, st.handle)
+        rc_ok = comm.all_reduce(send.ptr, recv.ptr, count, M.ncclFloat, M.ncclSum, st.handle)
+        st.sync()
+        got = recv.download(np.float32, count)
+        exp = O.allreduce(xs, "f32", "sum")[rank]
+        info = comm.info()
+        send.free()
+        recv.free()
+        st.destroy()
+        out_q.put((rank, {"rc_bad": rc_bad, "rc_ok": rc_ok, "bad": int((got.view(np.uint32) != exp.view(np.uint32)).sum()),
+                          "last_algo": info["last_algo"], "async": comm.async_error(), "destroy": comm.destroy()}))
     except Exception:
         out_q.put((rank, {"error": traceback.format_exc()}))
 

@@ -70,6 +70,10 @@ def _run_allreduce(n, cases, env=None, timeout=300, barrier=True):
             assert res["rc"] == 0, f"rank {r} case {c}: ncclResult {res['rc']}"
             assert res["bad"] == 0, f"rank {r} case {c}: {res['bad']} mismatches, first at {res['first']} {res.get('detail', '')}"
             assert res["async"] == 0
+            # the read schedule ran (no fallback) whenever every rank's buffers are device memory
+            dev_bufs = all(c.get(k, "device") == "device" for k in ("mem", "recv_mem"))
+            if c["algo"] == 2 and dev_bufs and c["count"] >= n:
+                assert res["last_algo"] == 2, f"rank {r} case {c}: ran schedule {res['last_algo']}"
     return out
 
 
@@ -79,7 +83,7 @@ def _case(dtype="f32", op="sum", count=1 << 18, inplace=False, algo=0, calls=1, 
                 offset=offset, **kw)
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 @pytest.mark.parametrize("n", [2, 3, 4])
 def test_allreduce_fp32_sum(dev, n, algo):
     cases = [
@@ -92,7 +96,7 @@ def test_allreduce_fp32_sum(dev, n, algo):
     _run_allreduce(n, cases)
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 @pytest.mark.parametrize("stage_host", ["0", "1"], ids=["mapped", "staged"])
 def test_host_buffers(dev, algo, stage_host):
     # the reference's perf_test hands cudaHostAlloc'd (pinned host) buffers straight to
@@ -112,7 +116,7 @@ def test_host_buffers(dev, algo, stage_host):
     _run_allreduce(3, cases, env={"MINI_NCCL_STAGE_HOST": stage_host})
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 @pytest.mark.parametrize("blocking", ["1", "0"], ids=["blocking", "async"])
 def test_skewed_ranks_varying_data(dev, algo, blocking):
     # injected delays (SURVEY.md §5 race detection): every rank sleeps 0-30 ms before each of
@@ -125,14 +129,17 @@ def test_skewed_ranks_varying_data(dev, algo, blocking):
 
 
 def test_auto_schedule_from_devices_no_init_allreduce(dev):
-    # MINI_NCCL_ALGO=auto (default): the schedule comes from the gathered device records, no
-    # all-reduce runs at init (tune_ms stays 0); every rank on one GPU -> ring at any n
+    # MINI_NCCL_ALGO=auto (default): the read schedule, with a scratch fallback that comes from
+    # the gathered device records (every rank on one GPU -> ring at any n); no all-reduce runs
+    # at init (tune_ms stays 0)
     port = GW.free_port()
     out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {}), 120)
     assert all("error" not in out[r] for r in range(3)), out
     for r in range(3):
         i = out[r]["info"]
-        assert i["tune_ms"] == [0.0, 0.0] and i["algo"] == 0 and i["ranks_on_device"] == 3, i
+        # auto = the read schedule; its fallback for buffers that cannot be shared: the ring here
+        assert i["tune_ms"] == [0.0, 0.0] and i["algo"] == 2 and i["scratch_algo"] == 0, i
+        assert i["ranks_on_device"] == 3 and i["last_algo"] == -1, i
         assert i["channels"] == 256 and i["pipelines"] == 256 and i["slot_bytes"] == 128 << 10
         assert i["scratch_bytes"] == 2 * 256 * 2 * (128 << 10)  # (n-1) peer regions
     port = GW.free_port()
@@ -153,7 +160,7 @@ def test_auto_tune_opt_in_picks_the_faster_schedule(dev):
     assert all(i["algo"] == (1 if t[1] <= t[0] else 0) for i in infos)
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 def test_sys_fence_on(dev, algo):
     # MINI_NCCL_SYS_FENCE=1: system release / acquire fences around every hand-off (the
     # default relies on sc0 sc1 payload accesses of uncached scratch instead)
@@ -161,7 +168,7 @@ def test_sys_fence_on(dev, algo):
     _run_allreduce(3, cases, env={"MINI_NCCL_SYS_FENCE": "1"})
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 def test_allreduce_8_ranks(dev, algo):
     # the 8-GPU node's rank count, all on GPU 0 at the library's default geometry (256
     # pipelines): every pair of the mesh exercised; BASELINE C3 (fp32) and C5 (fp16, bf16) on
@@ -180,7 +187,7 @@ def test_allreduce_8_ranks_c3_ring_128mib(dev):
     _run_allreduce(8, cases, timeout=600)
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 @pytest.mark.parametrize("n", [2, 4])
 @pytest.mark.parametrize("slice_kib", [64, 256, 1024])
 def test_allreduce_slice_points(dev, slice_kib, n, algo):
@@ -194,40 +201,66 @@ def test_allreduce_slice_points(dev, slice_kib, n, algo):
     _run_allreduce(n, cases, env={"MINI_NCCL_SLICE_SIZE": str(sl), "MINI_NCCL_CHANNELS": "16"}, timeout=600)
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 def test_allreduce_dtypes_ops(dev, algo):
     cases = [_case(dtype=d, op=o, count=50000 + 7 * i, algo=algo, seed=100 + i, special=o in ("max", "min"))
              for i, (d, o) in enumerate((d, o) for d in DTYPES for o in OPS)]
     _run_allreduce(3, cases)
 
 
+def test_read_schedule_count_mismatch_is_invalid_usage(dev):
+    # MINI_NCCL_ALGO=read: every rank sees every rank's (count, dtype, op) in the per-call
+    # rendezvous, so a call whose ranks disagree fails on all of them alike, and nothing is left
+    # half-done: the next (matching) call is bit-exact
+    port = GW.free_port()
+    env = {"MINI_NCCL_ALGO": "read", "MINI_NCCL_TIMEOUT_MS": "20000"}
+    out = GW.run_ranks(GW.mismatch_rank, 3, lambda r: (r, 3, port, env), 180)
+    for r in range(3):
+        assert "error" not in out[r], out[r].get("error")
+        o = out[r]
+        assert o["rc_bad"] == 5 and o["rc_ok"] == 0 and o["bad"] == 0 and o["last_algo"] == 2, o
+        assert o["async"] == 0 and o["destroy"] == 0
+
+
+def test_read_schedule_allocation_churn(dev):
+    # a fresh send and recv allocation for each of 70 calls (each freed after its call, so
+    # addresses come back with new allocation ids): every call maps the peers' new
+    # allocations, the per-process mapping cache stays bounded (64, least recently used out)
+    # and no stale mapping of a re-used address is ever read -- bit-exact each time
+    cases = [_case(count=4099 + 13 * i, algo=2, seed=900 + i, inplace=(i % 3 == 0)) for i in range(70)]
+    out = _run_allreduce(2, cases, timeout=600)
+    for r in range(2):
+        assert all(res["peer_mappings"] <= 64 for res in out[r]["results"])
+        assert out[r]["results"][-1]["peer_mappings"] >= 2
+
+
 def test_allreduce_c2_full_size(dev):
     # BASELINE.json configs[1] (C2): 2 ranks, 256 MiB fp32, MINI_NCCL_SLICE_SIZE = 128 KiB,
     # seeded uniform inputs, bit-exact against the oracle at full size
-    cases = [_case(count=64 << 20, algo=0, seed=1234)]
+    cases = [_case(count=64 << 20, algo=a, seed=1234 + a) for a in (0, 2)]
     _run_allreduce(2, cases, env={"MINI_NCCL_SLICE_SIZE": "131072"}, timeout=600)
 
 
 def test_allreduce_small_slices_many_messages(dev):
     # 1 KiB slices, 4 channels: thousands of flag hand-offs per call, both schedules
-    cases = [_case(count=(1 << 19) + 5, algo=a, calls=2, seed=77) for a in (0, 1)]
+    cases = [_case(count=(1 << 19) + 5, algo=a, calls=2, seed=77) for a in (0, 1, 2)]
     _run_allreduce(4, cases, env={"MINI_NCCL_SLICE_SIZE": "1024", "MINI_NCCL_CHANNELS": "4"})
 
 
 def test_allreduce_misaligned_buffers(dev):
     # dword-aligned but not 16-byte-aligned buffers (vector path with straddling vectors)
     # and 2-byte-aligned halves with odd chunks (element path)
-    cases = [_case(count=40001, algo=a, offset=o, seed=5) for a in (0, 1) for o in (4, 8, 12)]
-    cases += [_case(dtype="bf16", count=30001, algo=a, offset=2, seed=6) for a in (0, 1)]
+    cases = [_case(count=40001, algo=a, offset=o, seed=5) for a in (0, 1, 2) for o in (4, 8, 12)]
+    cases += [_case(dtype="bf16", count=30001, algo=a, offset=2, seed=6) for a in (0, 1, 2)]
     _run_allreduce(3, cases)
 
 
 def test_allreduce_async_mode(dev):
-    cases = [_case(count=1 << 20, algo=a, calls=4, seed=3) for a in (0, 1)]
+    cases = [_case(count=1 << 20, algo=a, calls=4, seed=3) for a in (0, 1, 2)]
     _run_allreduce(2, cases, env={"MINI_NCCL_BLOCKING": "0"})
 
 
-@pytest.mark.parametrize("algo", ["ring", "direct"])
+@pytest.mark.parametrize("algo", ["ring", "direct", "read"])
 def test_destroy_waits_for_calls_in_flight(dev, algo):
     port = GW.free_port()
     env = {"MINI_NCCL_BLOCKING": "0", "MINI_NCCL_ALGO": algo, "MINI_NCCL_TUNE": "0", "MINI_NCCL_TIMEOUT_MS": "30000"}
@@ -257,7 +290,7 @@ def test_watchdog_timeout_is_internal_error_and_sticky(dev):
     assert out[0]["async"] == M.ncclInternalError
 
 
-@pytest.mark.parametrize("algo", ["ring", "direct"])
+@pytest.mark.parametrize("algo", ["ring", "direct", "read"])
 def test_allreduce_hip_graph_capture_and_replay(dev, algo):
     # the reference only warns under capture (api.cpp:153-166); here a captured all-reduce
     # replays correctly because the FIFO counters are device state advanced by the kernel
@@ -272,7 +305,7 @@ def test_allreduce_hip_graph_capture_and_replay(dev, algo):
         assert out[r]["eager_rc"] == 0 and out[r]["eager_bad"] == 0
 
 
-@pytest.mark.parametrize("algo", ["ring", "direct"])
+@pytest.mark.parametrize("algo", ["ring", "direct", "read"])
 def test_calls_on_alternating_streams_are_ordered(dev, algo):
     port = GW.free_port()
     env = {"MINI_NCCL_TIMEOUT_MS": "20000", "MINI_NCCL_ALGO": algo, "MINI_NCCL_BLOCKING": "0", "MINI_NCCL_TUNE": "0"}
@@ -335,7 +368,7 @@ def test_watchdog_deadline_starts_with_the_kernel(dev):
         assert out[r]["secs"] >= 5.5 and out[r]["destroy"] == 0, out[r]
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 @pytest.mark.parametrize("n", [2, 3])
 def test_pull_placement(dev, algo, n):
     # MINI_NCCL_PULL=1: every slot in the sender's scratch, loaded by the receiver over the link

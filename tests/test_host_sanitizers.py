@@ -41,7 +41,7 @@ def _build_abi_selftest(tmp_path):
                        timeout=900)
     exe = str(tmp_path / "abi_selftest")
     srcs = [os.path.join(ROOT, "tests", "native", "abi_selftest.cpp")] + \
-        [os.path.join(CSRC, f) for f in ("api.cpp", "comm.cpp", "bootstrap.cpp", "config.cpp")]
+        [os.path.join(CSRC, f) for f in ("api.cpp", "comm.cpp", "peerbuf.cpp", "bootstrap.cpp", "config.cpp")]
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
            "-fno-sanitize-recover=undefined", "-Wno-unused-result", "-pthread", "-D__HIP_PLATFORM_AMD__",
            "-I/opt/rocm/include", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-o", exe] + srcs + \

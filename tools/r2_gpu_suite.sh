@@ -9,5 +9,5 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeou
   > gpurun_out/gpu_tests_$TAG.log 2>&1
 rc=$?
 tail -5 gpurun_out/gpu_tests_$TAG.log
-grep -E "PASSED|FAILED|ERROR" gpurun_out/gpu_tests_$TAG.log | awk '{print $NF}' | sort | uniq -c
+grep -E "PASSED|FAILED|ERROR" gpurun_out/gpu_tests_$TAG.log | awk '{print $(NF-1)}' | sort | uniq -c
 exit $rc
