@@ -520,7 +520,9 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.chunk_bytes = chunk_bytes;
   const int C = wave_channels();
   p.slot_bytes = wave_slice();
-  p.slice_bytes = effective_slice(chunk_bytes, C, wave_slice(), cfg_.min_slice, cfg_.pipe_depth);
+  p.slice_bytes = algo == 2 ? read_slice(chunk_bytes, C, cfg_.slice_size, cfg_.min_slice,
+                                         cfg_.pipe_depth > 1 ? cfg_.pipe_depth : kReadDepth)
+                            : effective_slice(chunk_bytes, C, wave_slice(), cfg_.min_slice, cfg_.pipe_depth);
   p.nslices = (chunk_bytes + p.slice_bytes - 1) / p.slice_bytes;
   p.iters = (uint32_t)((p.nslices + (uint64_t)C - 1) / (uint64_t)C);
   p.n = n;

@@ -141,6 +141,24 @@ MNCCL_HD uint64_t effective_slice(uint64_t chunk_bytes, int C, uint64_t slice, u
   return want < slice ? want : slice;
 }
 
+// Read schedule payload: no scratch slot bounds it, so it aims for kReadDepth iterations per
+// pipeline (a pipeline's first fold and last copy do not overlap anything: more, smaller
+// iterations shrink that fill and drain) while slices stay >= kReadMinSlice; below that, fewer
+// iterations of kReadMinSlice, down to the adaptive one-slice-per-pipeline payload of small
+// calls.  Measured on the one-GPU proxy, 1 GiB per rank (profiles/r2_read_depth_sweep.txt):
+// 4 ranks 508 -> 615 GB/s, 8 ranks 262 -> 301 GB/s, 2 ranks unchanged.  A pure function of the
+// call's size and the rank-uniform config, like effective_slice.
+constexpr int kReadDepth = 16;
+constexpr uint64_t kReadMinSlice = 16u << 10;
+MNCCL_HD uint64_t read_slice(uint64_t chunk_bytes, int C, uint64_t slice, uint64_t min_slice, int depth) {
+  uint64_t s = effective_slice(chunk_bytes, C, slice, min_slice, depth);
+  if (s < kReadMinSlice) {
+    const uint64_t one = effective_slice(chunk_bytes, C, slice, min_slice, 1);
+    s = one < kReadMinSlice ? one : kReadMinSlice;
+  }
+  return s;
+}
+
 // Scratch layout: one region per PEER rank (n - 1 of them: the owner never sends to itself),
 // [C][slots][slice_bytes] each.  region_index maps a peer rank q != owner to its region.
 MNCCL_HD uint64_t scratch_region_bytes(int C, int slots, uint64_t slice_bytes) { return (uint64_t)C * slots * slice_bytes; }

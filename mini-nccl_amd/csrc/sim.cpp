@@ -65,8 +65,8 @@ void do_move(int kind, int op, const float* local, const float* in, float* recv,
 struct Prog {
   int r, w;
   uint32_t it = 0;
-  int k = 0;      // ring: op index within the iteration
-  uint32_t j = 0; // direct: phase step (direct_phase_at)
+  int k = 0;      // ring: op index within the iteration; read: 0 = fold, 1..n-1 = copy from peer k
+  uint32_t j = 0; // direct: phase step (direct_phase_at); read: stage
   bool done = false;
 };
 
@@ -172,6 +172,81 @@ bool direct_step(World& W, Prog& P) {
   return true;
 }
 
+// One step of the read schedule (kernels.hip read_kernel): stage 0 publishes START, 1 waits for
+// every peer's START, 2 runs the iterations (k == 0: fold of iteration it from the peers' send
+// buffers into recv, then READY; k >= 1: copy of peer k's result slice of iteration it-1 out of
+// its recv, after its READY), 3 publishes DONE (+ credits), 4 waits for every peer's DONE.
+// Every peer access reads the peer's own buffers (W.send / W.recv of that rank), so an in-place
+// call whose order were wrong would read overwritten data and fail the oracle comparison.
+bool read_step(World& W, Prog& P) {
+  const int n = W.n, r = P.r, w = P.w;
+  auto tx = [&](int d) { return W.tx_seq[r][(size_t)d * W.C + w]; };
+  auto rx = [&](int q) { return W.rx_seq[r][(size_t)q * W.C + w]; };
+  const uint64_t mpc = read_msgs_per_call(W.iters);
+  switch (P.j) {
+    case 0:
+      for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx(direct_peer(n, r, k)) + 1;
+      P.j = 1;
+      return true;
+    case 1:
+      for (int k = 1; k < n; ++k)
+        if (W.ready(r, direct_peer(n, r, k), w) < rx(direct_peer(n, r, k)) + 1) return false;
+      P.j = 2;
+      P.it = 0;
+      P.k = 0;
+      return true;
+    case 2: {
+      if (P.k == 0) {
+        if (P.it < W.iters) {
+          const uint64_t s = (uint64_t)P.it * W.C + w;
+          const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
+          const uint64_t coff = (uint64_t)r * W.chunk_bytes + s * W.slice;
+          const float* local = (const float*)((const char*)W.send[r] + coff);
+          float* out = (float*)((char*)W.recv[r] + coff);
+          for (uint64_t i = 0; i < len / 4; ++i) {
+            float acc = local[i];
+            for (int k = 1; k < n; ++k) {
+              const int q = direct_peer(n, r, k);
+              acc = apply(W.op, ((const float*)((const char*)W.send[q] + coff))[i], acc);
+            }
+            out[i] = acc;
+          }
+          for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx(direct_peer(n, r, k)) + 2 + P.it;
+        }
+        if (P.it > 0) P.k = 1;
+        else ++P.it;
+      } else {
+        const uint32_t t = P.it - 1;
+        const int q = direct_peer(n, r, 1 + (P.k - 1 + w) % (n - 1));
+        if (W.ready(r, q, w) < rx(q) + 2 + t) return false;
+        const uint64_t s = (uint64_t)t * W.C + w;
+        const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
+        const uint64_t coff = (uint64_t)q * W.chunk_bytes + s * W.slice;
+        memcpy((char*)W.recv[r] + coff, (const char*)W.recv[q] + coff, len);
+        if (++P.k == n) {
+          P.k = 0;
+          ++P.it;
+        }
+      }
+      if (P.it > W.iters) P.j = 3;
+      return true;
+    }
+    case 3:
+      for (int k = 1; k < n; ++k) {
+        const int q = direct_peer(n, r, k);
+        W.credit(q, r, w) = rx(q) + mpc;
+        W.ready(q, r, w) = tx(q) + mpc;
+      }
+      P.j = 4;
+      return true;
+    default:
+      for (int k = 1; k < n; ++k)
+        if (W.ready(r, direct_peer(n, r, k), w) < rx(direct_peer(n, r, k)) + mpc) return false;
+      P.done = true;
+      return true;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -194,12 +269,17 @@ void mnccl_pipeline_geometry(int n, int channels, int threads, int window, int s
   out[3] = g.scratch_bytes;
 }
 
-// Runs `calls` consecutive all-reduces (send -> recv, fp32) on n simulated ranks with the
-// GPU kernels' protocol; call i uses schedule (algo >> i) & 1 (so schedules can alternate
-// on one communicator state, as mncclCommSetAlgo allows).  schedule_seed != 0 permutes the order programs are tried in
+uint64_t mnccl_read_slice(uint64_t chunk_bytes, int channels, uint64_t slice, uint64_t min_slice, int depth) {
+  return read_slice(chunk_bytes, channels, slice, min_slice, depth);
+}
+
+// Runs `calls` consecutive all-reduces (send -> recv, fp32; send == recv for in place) on n
+// simulated ranks with the GPU kernels' protocol; call i uses schedule (algo >> 2i) & 3 (0 ring,
+// 1 direct, 2 read; schedules can alternate on one communicator state, as mncclCommSetAlgo
+// allows).  schedule_seed != 0 permutes the order programs are tried in
 // (pseudo-random), exploring different interleavings.  Returns 0, -1 on deadlock,
 // -2 on bad arguments.  *steps_out = ops executed.
-int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, int n, uint64_t count, int op,
+int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* recv, int n, uint64_t count, int op,
                         uint64_t slice_bytes, uint64_t min_slice, int direct_overlap, int pull, int channels,
                         int slots, int calls, uint64_t schedule_seed, uint64_t* steps_out) {
   if (n < 1 || n > 16 || channels < 1 || slots < 1 || slice_bytes < 4 || slice_bytes % 4) return -2;
@@ -209,10 +289,6 @@ int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, 
   W.pull = pull;
   const uint64_t chunk = count / (uint64_t)n;
   W.chunk_bytes = chunk * 4;
-  // as Comm::launch_ring_or_direct: adaptive payload (min_slice 0 = off), fixed slot stride
-  W.slice = min_slice ? effective_slice(W.chunk_bytes, channels, slice_bytes, min_slice, 1) : slice_bytes;
-  W.nslices = (W.chunk_bytes + W.slice - 1) / W.slice;
-  W.iters = (uint32_t)((W.nslices + (uint64_t)channels - 1) / (uint64_t)channels);
   W.send.assign(send, send + n);
   W.recv.assign(recv, recv + n);
   // n - 1 regions per rank, exactly as Comm allocates (schedule.h region_index)
@@ -223,8 +299,16 @@ int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, 
   uint64_t steps = 0;
   uint64_t rng = schedule_seed * 6364136223846793005ull + 1442695040888963407ull;
   for (int call = 0; call < calls; ++call) {
-    const int a = (algo >> call) & 1;
+    const int a = (int)((algo >> (2 * call)) & 3);
+    // as Comm::launch: adaptive payload (min_slice 0 = off; the read schedule's own rule), fixed
+    // slot stride
+    if (!min_slice) W.slice = slice_bytes;
+    else if (a == 2) W.slice = read_slice(W.chunk_bytes, channels, slice_bytes, min_slice, kReadDepth);
+    else W.slice = effective_slice(W.chunk_bytes, channels, slice_bytes, min_slice, 1);
+    W.nslices = (W.chunk_bytes + W.slice - 1) / W.slice;
+    W.iters = (uint32_t)((W.nslices + (uint64_t)channels - 1) / (uint64_t)channels);
     for (int r = 0; r < n; ++r) {  // send -> recv copy of the tail (Comm::allreduce)
+      if ((const void*)recv[r] == (const void*)send[r]) continue;  // in place
       const uint64_t body = W.chunk_bytes * (uint64_t)n;
       if (n == 1 || chunk == 0) memcpy(recv[r], send[r], count * 4);
       else if (count * 4 > body) memcpy((char*)recv[r] + body, (const char*)send[r] + body, count * 4 - body);
@@ -253,7 +337,7 @@ int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, 
           burst = 1 + (int)((rng >> 40) % 4);
         }
         for (int b = 0; b < burst && !P.done; ++b) {
-          const bool ok = a == 1 ? direct_step(W, P) : ring_step(W, P);
+          const bool ok = a == 2 ? read_step(W, P) : a == 1 ? direct_step(W, P) : ring_step(W, P);
           if (!ok) break;
           any = true;
           ++steps;
@@ -266,7 +350,13 @@ int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, 
     // the kernels' last action per channel: advance the per-pair FIFO counters
     for (int r = 0; r < n; ++r)
       for (int w = 0; w < channels; ++w) {
-        if (a == 1) {
+        if (a == 2) {
+          for (int q = 0; q < n; ++q) {
+            if (q == r) continue;
+            W.tx_seq[r][(size_t)q * channels + w] += read_msgs_per_call(W.iters);
+            W.rx_seq[r][(size_t)q * channels + w] += read_msgs_per_call(W.iters);
+          }
+        } else if (a == 1) {
           for (int q = 0; q < n; ++q) {
             if (q == r) continue;
             W.tx_seq[r][(size_t)q * channels + w] += (uint64_t)W.iters * direct_msgs_per_iter();

@@ -18,8 +18,10 @@ def load():
     if _lib is None:
         L = ctypes.CDLL(LIB)
         vp, u64, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
-        L.mnccl_sim_allreduce.argtypes = [i, ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64, u64, i, i, i, i, i, u64,
-                                          ctypes.POINTER(u64)]
+        L.mnccl_sim_allreduce.argtypes = [u64, ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64, u64, i, i, i, i, i,
+                                          u64, ctypes.POINTER(u64)]
+        L.mnccl_read_slice.argtypes = [u64, i, u64, u64, i]
+        L.mnccl_read_slice.restype = u64
         L.mnccl_direct_phase_at.argtypes = [ctypes.c_uint32, ctypes.c_uint32, i, ctypes.POINTER(i),
                                             ctypes.POINTER(ctypes.c_uint32)]
         L.mnccl_effective_slice.argtypes = [u64, i, u64, u64, i]
@@ -32,18 +34,20 @@ def load():
 
 
 def allreduce(inputs, algo=0, op=0, slice_bytes=1024, channels=4, slots=2, calls=1, seed=0, algos=None, min_slice=0,
-              direct_overlap=1, pull=0):
+              direct_overlap=1, pull=0, inplace=False):
     """fp32 all-reduce of `inputs` (one array per rank) through the simulated kernels,
-    `calls` times on one communicator state (schedule `algo` for every call, or the
-    per-call list `algos`).  Returns (outputs, steps); raises RuntimeError on deadlock."""
-    if algos is not None:
-        calls = len(algos)
-        mask = sum((a & 1) << i for i, a in enumerate(algos))
-    else:
-        mask = (1 << calls) - 1 if algo == 1 else 0
+    `calls` times on one communicator state (schedule `algo` -- 0 ring, 1 direct, 2 read -- for
+    every call, or the per-call list `algos`; at most 32 calls).  inplace: send == recv (then
+    every call after the first reduces the previous result).  Returns (outputs, steps); raises
+    RuntimeError on deadlock."""
+    if algos is None:
+        algos = [algo] * calls
+    calls = len(algos)
+    assert calls <= 32
+    mask = sum((a & 3) << (2 * i) for i, a in enumerate(algos))
     n = len(inputs)
-    sends = [np.ascontiguousarray(x, dtype=np.float32) for x in inputs]
-    recvs = [np.full_like(x, np.nan) for x in sends]
+    sends = [np.array(x, dtype=np.float32) for x in inputs]  # own copies (in place writes them)
+    recvs = sends if inplace else [np.full_like(x, np.nan) for x in sends]
     sp = (ctypes.c_void_p * n)(*[s.ctypes.data for s in sends])
     rp = (ctypes.c_void_p * n)(*[r.ctypes.data for r in recvs])
     steps = ctypes.c_uint64()
@@ -74,6 +78,10 @@ def pipeline_geometry(n, channels=0, threads=64, window=64, signal_batch=16, slo
 
 def effective_slice(chunk_bytes, channels, slice_bytes, min_slice, depth=1):
     return load().mnccl_effective_slice(chunk_bytes, channels, slice_bytes, min_slice, depth)
+
+
+def read_slice(chunk_bytes, channels, slice_bytes, min_slice, depth=16):
+    return load().mnccl_read_slice(chunk_bytes, channels, slice_bytes, min_slice, depth)
 
 
 def direct_phase_at(j, iters, overlap):

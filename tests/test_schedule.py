@@ -20,7 +20,7 @@ def same_bits(a, b):
     return np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
 @pytest.mark.parametrize("count,slice_bytes,channels,slots", [
     (4096, 256, 4, 2),      # several slices per channel
@@ -37,7 +37,7 @@ def test_sim_matches_oracle(oracle_lib, sim_lib, algo, n, count, slice_bytes, ch
         assert same_bits(got[r], ref[r]), f"rank {r}"
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 @pytest.mark.parametrize("op", OPS)
 def test_sim_all_ops(oracle_lib, sim_lib, algo, op):
     xs = O.random_inputs(4, 2050, "f32", seed=11)
@@ -46,7 +46,7 @@ def test_sim_all_ops(oracle_lib, sim_lib, algo, op):
     assert all(same_bits(g, e) for g, e in zip(got, ref))
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 @pytest.mark.parametrize("seed", range(1, 13))
 def test_sim_random_interleavings_no_deadlock(oracle_lib, sim_lib, algo, seed):
     n = 2 + seed % 7
@@ -57,7 +57,7 @@ def test_sim_random_interleavings_no_deadlock(oracle_lib, sim_lib, algo, seed):
     assert all(same_bits(g, e) for g, e in zip(got, ref))
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 def test_sim_sequence_continues_across_calls(oracle_lib, sim_lib, algo):
     # 5 calls on one communicator state: flags are monotone and never reset
     xs = O.random_inputs(4, 5000, "f32", seed=5)
@@ -86,7 +86,7 @@ def test_single_slot_fifo_deadlocks(sim_lib, algo):
         S.allreduce(xs, algo=algo, slice_bytes=256, channels=2, slots=1)
 
 
-@pytest.mark.parametrize("algos", [[0, 1, 0, 1], [1, 1, 0, 0, 1], [0, 0, 1]])
+@pytest.mark.parametrize("algos", [[0, 1, 0, 1], [1, 1, 0, 0, 1], [0, 0, 1], [2, 0, 2, 1, 2], [1, 2, 2, 0]])
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
 def test_sim_switching_schedules_on_one_communicator(oracle_lib, sim_lib, algos, n):
     # mncclCommSetAlgo between calls: per-pair FIFO counters keep every link consistent
@@ -114,7 +114,7 @@ def test_effective_slice_properties(sim_lib, chunk, C):
     assert S.effective_slice(chunk, C, slice_bytes, slice_bytes) == slice_bytes  # MIN_SLICE >= SLICE: off
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
 @pytest.mark.parametrize("n,count,seed", [(2, 70001, 1), (3, 40000, 2), (4, 9000, 3), (8, 123457, 4)])
 def test_sim_adaptive_slice(oracle_lib, sim_lib, algo, n, count, seed):
     # payload shrunk below the slot stride, random interleavings over 3 calls: same bits
@@ -162,3 +162,47 @@ def test_sim_pull_placement(oracle_lib, sim_lib, algo, seed):
     got, _ = S.allreduce(xs, algo=algo, slice_bytes=64, channels=1 + seed % 3, slots=2 + seed % 2, calls=3,
                          seed=seed, pull=1)
     assert all(same_bits(g, e) for g, e in zip(got, ref))
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("seed", range(1, 7))
+def test_sim_read_in_place_random_interleavings(oracle_lib, sim_lib, n, seed):
+    # the read schedule in place (send == recv): a rank overwrites its chunk q only after q's
+    # READY for that slice, i.e. after q has loaded its raw input from it; under random
+    # interleavings any earlier write would leave a wrong value behind
+    xs = O.random_inputs(n, 3000 + 7 * seed, "f32", seed=seed)
+    ref = O.allreduce(xs, slice_bytes=64)
+    got, _ = S.allreduce(xs, algo=2, slice_bytes=64, channels=1 + seed % 4, calls=1, seed=seed, inplace=True)
+    assert all(same_bits(g, e) for g, e in zip(got, ref))
+
+
+def test_sim_read_needs_no_slots(oracle_lib, sim_lib):
+    # no scratch FIFO: even one slot (which deadlocks the scratch schedules) is irrelevant
+    xs = O.random_inputs(3, 4096, "f32", seed=3)
+    got, _ = S.allreduce(xs, algo=2, slice_bytes=256, channels=2, slots=1)
+    assert all(same_bits(g, e) for g, e in zip(got, O.allreduce(xs, slice_bytes=256)))
+
+
+def test_read_message_counts(sim_lib):
+    # per pipeline and call: START, fold + (n-1) copies per iteration, DONE (publish + wait)
+    n, C = 4, 2
+    xs = O.random_inputs(n, n * 64, "f32")
+    _, steps = S.allreduce(xs, algo=2, slice_bytes=64, channels=C)
+    iters = -(-(64 * 4 // 64) // C)
+    assert steps == n * C * (4 + iters + 1 + iters * (n - 1))
+
+
+@pytest.mark.parametrize("chunk", [0, 4, 1000, 1 << 16, (1 << 20) + 12, 3 << 22, 1 << 27, 1 << 30])
+@pytest.mark.parametrize("C", [1, 7, 256])
+def test_read_slice_properties(sim_lib, chunk, C):
+    # the read schedule's payload (csrc/schedule.h read_slice): never above the configured slice;
+    # >= 16 iterations per pipeline while slices stay >= 16 KiB; otherwise 16 KiB or the
+    # one-slice-per-pipeline payload of small calls, whichever is smaller
+    sl, floor = 128 * 1024, 1024
+    e = S.read_slice(chunk, C, sl, floor)
+    assert floor <= e <= sl and (e == sl or e % 1024 == 0)
+    per_pipe = -(-chunk // C)
+    if per_pipe >= 16 * 16384:
+        assert -(-per_pipe // e) >= 16 or e == sl and -(-per_pipe // e) >= 1
+    if e < 16384:
+        assert e == S.effective_slice(chunk, C, sl, floor)

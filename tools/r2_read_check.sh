@@ -28,9 +28,13 @@ run() {
   if [ $rc -ne 0 ]; then cat /tmp/ps_0.log | tail -5; exit 9; fi
   return 0
 }
+IFS=';' read -ra VARS <<< "${VARIANTS:-}"
+[ ${#VARIANTS} -eq 0 ] && VARS=("")
 for n in ${NRS:-2 4 8}; do
   for a in ${ALGOS:-ring direct read}; do
-    run $n "$a" MINI_NCCL_ALGO=$a $EXTRA
+    for v in "${VARS[@]}"; do
+      run $n "$a $v" MINI_NCCL_ALGO=$a $v
+    done
   done
 done
 echo read-check-done
