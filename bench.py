@@ -751,7 +751,8 @@ def main():
                 if rank == 0:
                     arm(result)
             comm.set_algo(ALGO_NAMES.index(args.algo))
-        traffic, tsrc = pmc_traffic(f"{args.algo}_{args.dtype}_1GiB_n{n}")
+        # rank 0's kernel, measured where this run runs (ranks sharing one GPU: the proxy entry)
+        traffic, tsrc = pmc_traffic(f"{args.algo}_{args.dtype}_1GiB_n{n}" + ("_same_gpu" if args.same_device else ""))
         kern_key = f"{args.algo}_kernel"
     achieved = alg_bytes / (ev_ms / 1e3) / 1e9
     result["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

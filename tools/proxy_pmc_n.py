@@ -38,7 +38,8 @@ def main():
     tag, rnd, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
     algos = sys.argv[4:] or ["ring", "direct"]
     base = os.path.join(ROOT, "gpurun_out", tag)
-    fused = 4 * (COUNT // n) * (6 * n - 4)
+    def fused_of(algo):  # bench.py fused_bytes: read has no scratch
+        return 4 * (COUNT // n) * ((3 * n - 1) if algo == "read" else (6 * n - 4))
     summ_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     summ = json.load(open(summ_path)) if os.path.exists(summ_path) else {}
     pmc_csv = os.path.join(ROOT, "profiles", f"{rnd}_proxy_pmc_n{n}.csv")
@@ -49,6 +50,7 @@ def main():
         ws.writerow(["Algo", "Kernel_Name", "Calls", "median_ns_after_first_5", "MinNs", "MaxNs",
                      "fused_alg_bytes", "fused_GBps_one_rank", "ranks_x_fused_GBps"])
         for algo in algos:
+            fused = fused_of(algo)
             k = f"{algo}_kernel"
             tr = rows(os.path.join(base, f"trace_{algo}_n{n}", "run_kernel_trace.csv"), k)
             durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr]
@@ -69,7 +71,8 @@ def main():
                 "kernel_median_ns": int(md),
                 "dispatches": [len(fe), len(wr)],
                 "note": f"{n} ranks sharing ONE MI355X (proxy); rank 0 profiled (apps/bin/perf_test --sizes 1024, "
-                        "MINI_NCCL_TUNE=0); medians after the first 5 dispatches; fused bytes = 4 B x chunk x (6n-4)",
+                        "default knobs); medians after the first 5 dispatches; fused bytes = 4 B x chunk x (6n-4) for "
+                        "ring / direct, x (3n-1) for read",
                 "source": f"profiles/{rnd}_proxy_pmc_n{n}.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate "
                           "passes; FETCH x2, KiB x1024)",
             }
