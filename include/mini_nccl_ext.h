@@ -35,8 +35,8 @@ typedef enum {
                           their send buffers (mapped per allocation, negotiated per call),
                           folds them in the same order into its recv, and every peer loads
                           the result from there; a call whose buffers some rank cannot share
-                          (host memory, graph capture) runs the scratch schedule instead, on
-                          every rank alike */
+                          (host memory) runs the scratch schedule instead, on every rank
+                          alike */
 } mncclAlgo_t;
 
 typedef struct {

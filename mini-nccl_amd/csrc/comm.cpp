@@ -629,14 +629,15 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     const char* precv[kMaxRanks] = {};
     if (algo_ == 2 && pbuf_.available()) {
       // the read schedule: every rank takes part in the rendezvous, all decide alike
-      const bool eligible = !capturing && ksend == send && krecv == recv && device_local(send) && device_local(recv);
+      // a captured call reads through mappings its replays keep using: they are pinned
+      const bool eligible = ksend == send && krecv == recv && device_local(send) && device_local(recv);
       bool vec_all = false;
       PeerBuffers::Decision d = PeerBuffers::kFallback;
       try {
         // a peer that does not reach the call within the watchdog's limit fails it, as the
         // kernel's own wait would (the reference's 10 s watchdog, mini_nccl.cu:200-214)
         d = pbuf_.negotiate(send, recv, eligible, count, dtype, op, cfg_.timeout_ms / 1000.0 + 2.0,
-                            [this] { wait_previous_call(); }, psend, precv, &vec_all);
+                            [this] { wait_previous_call(); }, psend, precv, &vec_all, capturing);
       } catch (const std::exception& e) {
         fprintf(stderr, "[Mini-NCCL] rank %d: %s; communicator is no longer usable\n", rank_, e.what());
         sticky_ = ncclInternalError;

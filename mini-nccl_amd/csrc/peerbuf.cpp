@@ -139,17 +139,20 @@ bool PeerBuffers::describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMe
 }
 
 char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h,
-                            const std::function<void()>& sync_previous) {
+                            const std::function<void()>& sync_previous, bool pin) {
   for (Mapping& m : peers_)
     if (m.rank == q && m.base == base && m.id == id) {
       m.last_use = seq_;
+      m.pinned = m.pinned || pin;
       return m.local;
     }
-  if (peers_.size() >= kMaxMappings) {
-    // least recently used out; the last kernel may still read through it
-    size_t lru = 0;
-    for (size_t i = 1; i < peers_.size(); ++i)
-      if (peers_[i].last_use < peers_[lru].last_use) lru = i;
+  size_t unpinned = 0;
+  for (const Mapping& m : peers_) unpinned += m.pinned ? 0 : 1;
+  if (unpinned >= kMaxMappings) {
+    // least recently used (unpinned) out; the last kernel may still read through it
+    size_t lru = peers_.size();
+    for (size_t i = 0; i < peers_.size(); ++i)
+      if (!peers_[i].pinned && (lru == peers_.size() || peers_[i].last_use < peers_[lru].last_use)) lru = i;
     sync_previous();
     hipIpcCloseMemHandle(peers_[lru].local);
     peers_.erase(peers_.begin() + (long)lru);
@@ -161,7 +164,7 @@ char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHa
     throw std::runtime_error(std::string("read schedule: hipIpcOpenMemHandle of rank ") + std::to_string(q) +
                              "'s buffer: " + hipGetErrorString(e));
   }
-  peers_.push_back(Mapping{q, base, id, (char*)p, seq_});
+  peers_.push_back(Mapping{q, base, id, (char*)p, seq_, pin});
   return (char*)p;
 }
 
@@ -174,7 +177,7 @@ void PeerBuffers::close_all() {
 PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv, bool eligible, uint64_t count,
                                              int dtype, int op, double timeout_s,
                                              const std::function<void()>& sync_previous, const char** psend,
-                                             const char** precv, bool* vec_all) {
+                                             const char** precv, bool* vec_all, bool pin) {
   const uint64_t k = ++seq_;
   const int slot = (int)(k % kBoardDepth);
   const double t0 = now_s();
@@ -236,8 +239,8 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
       precv[q] = (const char*)(uintptr_t)c.recv.raw;
       continue;
     }
-    psend[q] = map_peer(q, c.send.base, c.send.id, c.send.h, sync_previous) + c.send.off;
-    precv[q] = map_peer(q, c.recv.base, c.recv.id, c.recv.h, sync_previous) + c.recv.off;
+    psend[q] = map_peer(q, c.send.base, c.send.id, c.send.h, sync_previous, pin) + c.send.off;
+    precv[q] = map_peer(q, c.recv.base, c.recv.id, c.recv.h, sync_previous, pin) + c.recv.off;
   }
   *vec_all = aligned;
   return d;

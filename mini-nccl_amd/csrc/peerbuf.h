@@ -43,14 +43,15 @@ class PeerBuffers {
   bool available() const { return board_ != nullptr; }
 
   enum Decision { kRead = 1, kFallback = 0, kMismatch = -1 };
-  // One call's rendezvous.  `eligible`: this rank's buffers are device memory of this GPU and
-  // the call is not being captured.  On kRead, psend / precv[q] hold rank q's buffers mapped
+  // One call's rendezvous.  `eligible`: this rank's buffers are device memory of this GPU.  On kRead, psend / precv[q] hold rank q's buffers mapped
   // here (this rank's own at [rank]) and *vec_all whether every rank's buffers are dword-aligned.
   // `sync_previous` waits for this communicator's last kernel (before a cached mapping is
   // closed).  Throws std::runtime_error when a peer does not arrive within timeout_s.
+  // `pin`: the call is being captured into a graph whose replays will read through these
+  // mappings: they are never evicted (closed only with the communicator).
   Decision negotiate(const void* send, const void* recv, bool eligible, uint64_t count, int dtype, int op,
                      double timeout_s, const std::function<void()>& sync_previous, const char** psend,
-                     const char** precv, bool* vec_all);
+                     const char** precv, bool* vec_all, bool pin = false);
   // Unmaps every peer allocation; call when no kernel of this communicator can still run.
   void close_all();
 
@@ -67,10 +68,11 @@ class PeerBuffers {
     uint64_t base, id;  // in the owner's process
     char* local;        // the allocation base mapped here
     uint64_t last_use;
+    bool pinned;        // used by a captured graph: never evicted
   };
   bool describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMemHandle_t* h);
   char* map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h,
-                 const std::function<void()>& sync_previous);
+                 const std::function<void()>& sync_previous, bool pin);
 
   Board* board_ = nullptr;
   size_t board_bytes_ = 0;

@@ -149,6 +149,7 @@ def graph_rank(rank, n, port, env, replays, out_q):
         rcs = []
         g = hip_rt.Graph(st, lambda: rcs.append(comm.all_reduce(send.ptr, recv.ptr, count, M.ncclFloat, M.ncclSum,
                                                                 st.handle)))
+        captured_algo = comm.info()["last_algo"]  # the schedule baked into the graph
         bad = []
         for k in range(replays):
             xs = O.random_inputs(n, count, "f32", seed=500 + k)
@@ -166,7 +167,7 @@ def graph_rank(rank, n, port, env, replays, out_q):
         got = recv.download(np.float32, count)
         exp = O.allreduce(xs, "f32", "sum")[rank]
         g.destroy()
-        out_q.put((rank, {"capture_rc": rcs, "bad": bad, "eager_rc": rc,
+        out_q.put((rank, {"capture_rc": rcs, "bad": bad, "eager_rc": rc, "captured_algo": captured_algo,
                           "eager_bad": int((got.view(np.uint32) != exp.view(np.uint32)).sum())}))
         send.free()
         recv.free()

@@ -303,6 +303,8 @@ def test_allreduce_hip_graph_capture_and_replay(dev, algo):
         assert out[r]["capture_rc"] == [0]
         assert out[r]["bad"] == [0, 0, 0, 0]
         assert out[r]["eager_rc"] == 0 and out[r]["eager_bad"] == 0
+        # the read schedule is captured too (its peer mappings pinned for the replays)
+        assert out[r]["captured_algo"] == {"ring": 0, "direct": 1, "read": 2}[algo]
 
 
 @pytest.mark.parametrize("algo", ["ring", "direct", "read"])

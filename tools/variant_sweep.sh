@@ -8,7 +8,7 @@ run() {
   local port=$((20000 + RANDOM % 20000))
   local pids=()
   for ((r = 1; r < NR; r++)); do
-    env "$@" LD_LIBRARY_PATH=$lib MINI_NCCL_PORT=$port MINI_NCCL_PERF_DEVICE=0 timeout -k 5 60 $R/apps/bin/perf_test $r $NR --sizes $SIZE --iters 10 --warmup 3 > /tmp/vs_$r.log 2>&1 &
+    env "$@" GPU_MAX_HW_QUEUES=2 LD_LIBRARY_PATH=$lib MINI_NCCL_PORT=$port MINI_NCCL_PERF_DEVICE=0 timeout -k 5 60 $R/apps/bin/perf_test $r $NR --sizes $SIZE --iters 10 --warmup 3 > /tmp/vs_$r.log 2>&1 &
     pids+=($!)
   done
   env "$@" LD_LIBRARY_PATH=$lib MINI_NCCL_PORT=$port MINI_NCCL_PERF_DEVICE=0 timeout -k 5 60 $R/apps/bin/perf_test 0 $NR --sizes $SIZE --iters 10 --warmup 3 > /tmp/vs_0.log 2>&1
