@@ -158,8 +158,10 @@ C4_WINDOWS = [16, 32, 64]
 C4_COUNT = int(os.environ.get("MNCCL_BENCH_C4_MIB", "4096")) * (1 << 20) // 4
 
 
-def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_ranks):
+def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_ranks, dtype="f32"):
     """one communicator with `env` knobs; returns algbw GB/s (max time over ranks) and check"""
+    tdt, ndt, esz = {"f32": (torch.float32, M.ncclFloat, 4), "bf16": (torch.bfloat16, M.ncclBfloat16, 2),
+                     "f16": (torch.float16, M.ncclFloat16, 2)}[dtype]
     env = dict(env, MINI_NCCL_TUNE=0)  # the point sets its schedule itself
     saved = {k: os.environ.get(k) for k in env}
     os.environ.update({k: str(v) for k, v in env.items()})
@@ -168,11 +170,11 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
         comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
         comm.set_algo(ALGO_NAMES.index(algo))
         st = torch.cuda.Stream(device=dev)
-        send = torch.ones(count, device=dev, dtype=torch.float32)
-        recv = torch.empty(count, device=dev, dtype=torch.float32)
+        send = torch.ones(count, device=dev, dtype=tdt)
+        recv = torch.empty(count, device=dev, dtype=tdt)
 
         def call():
-            rc = comm.all_reduce(send.data_ptr(), recv.data_ptr(), count, M.ncclFloat, M.ncclSum, st.cuda_stream)
+            rc = comm.all_reduce(send.data_ptr(), recv.data_ptr(), count, ndt, M.ncclSum, st.cuda_stream)
             if rc != 0:
                 raise M.NcclError(rc, "ncclAllReduce")
 
@@ -185,11 +187,11 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
         torch.cuda.synchronize()
         dt = max_over_ranks(time.perf_counter() - t0)
         ok = comm.async_error() == 0 and bool((recv == float(n)).all().item())
-        ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, torch.float32, M.ncclFloat, st, 1)
+        ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, st, 1)
         i = comm.info()
         ok = ok and i["last_algo"] == ALGO_NAMES.index(algo)  # the point ran its own schedule
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
-        return {"GBps": round(count * 4 / (dt / reps) / 1e9, 2), "ok": ok, "workgroups": i["channels"],
+        return {"GBps": round(count * esz / (dt / reps) / 1e9, 2), "ok": ok, "workgroups": i["channels"],
                 "pipelines": i["pipelines"], "slot_bytes": i["slot_bytes"], "scratch_MiB": i["scratch_bytes"] >> 20}
     except Exception as e:
         return {"error": str(e)[:120]}
@@ -258,6 +260,10 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
                                                    max_over_ranks)
         out["c4_direct_4GiB_defaults"] = sweep_point(M, torch, dist, dev, n, rank, {}, "direct", C4_COUNT, 3,
                                                      max_over_ranks)
+        # BASELINE.json configs[4] (C5): 1 GiB of bf16 / fp16 per rank, library defaults; the
+        # check is exact (integer-valued sums stay exact in 2-byte floats)
+        out["c5_read_1GiB"] = {dt: sweep_point(M, torch, dist, dev, n, rank, {}, "read", (1 << 30) // 2, 5,
+                                               max_over_ranks, dtype=dt) for dt in ("bf16", "f16")}
     return out
 
 
