@@ -9,6 +9,8 @@
 //                 rank's scratch with epoch-free monotone flags and explicit credits.
 //                 Default geometry: 256 one-wave workgroups = one pipeline per CU.
 //  direct_kernel  same association order, every peer link at once (schedule.h).
+//  read_kernel    the default: same association order, no scratch -- each rank loads its
+//                 peers' send / recv buffers over the links (mapped by Comm per allocation).
 //  local_reduce   the element-wise op alone: out = op(local, incoming), 16 B per lane.
 //
 // Memory-ordering protocol (cross-process, cross-device over xGMI):
@@ -31,6 +33,10 @@
 //    consistent); nothing is reset per call and stale flags cannot satisfy a wait.
 //  * every spin is bounded (MINI_NCCL_TIMEOUT_MS via s_memrealtime) and also exits on
 //    the host abort word or a peer's ABORT; the kernel always terminates.
+//  * read_kernel loads the peers' user buffers with the same sc0 sc1 loads, after their START
+//    (their send is in memory: every kernel before the call ended and wrote its data back)
+//    or READY (their result slice was stored sc0 sc1 and drained before the flag); its own
+//    result slices are stored sc0 sc1 for the peers' loads.
 //  * MINI_NCCL_PULL=1 moves the slots to the sender's scratch (schedule.h slot_owner): the
 //    producer's sc0 sc1 stores stay local, the consumer's sc0 sc1 loads cross the link; the
 //    flags, credits and the drain-before-flag order are unchanged, and so is the argument
@@ -653,6 +659,19 @@ __device__ __forceinline__ void read_fold_scalar(const CollParams& p, uint64_t c
   }
 }
 
+// Vectors per lane per batch of the read kernel: 16 in the fold (two peers' 16 KiB in flight
+// per wave) and 32 in the copies (32 KiB per wave).  Latency insurance for loads that cross
+// xGMI: a wave's rate is its bytes in flight over the load's round trip, so twice the scratch
+// kernels' batches halve the pipelines a link needs to stay busy; measured free on the one-GPU
+// proxy (2 / 4 / 8 ranks, profiles/r2_read_batch_variants.txt), no VGPR spill (217 VGPRs).
+#ifndef MNCCL_READ_FOLD_U
+#define MNCCL_READ_FOLD_U 16
+#endif
+#ifndef MNCCL_READ_COPY_U
+#define MNCCL_READ_COPY_U 32
+#endif
+constexpr int kReadFoldU = MNCCL_READ_FOLD_U, kReadCopyU = MNCCL_READ_COPY_U;
+
 template <typename T, int OPC, bool VEC>
 __device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, uint32_t nbytes, int lane) {
   if (!VEC) {
@@ -660,7 +679,7 @@ __device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, ui
     return;
   }
   const int n = p.n, r = p.rank;
-  constexpr int U = kFoldU;
+  constexpr int U = kReadFoldU;
   const rsrc_t out = make_rsrc(p.recv + coff, nbytes);
   const char* lsrc = p.send + coff;
   const uint32_t nvec = nbytes >> 4;
@@ -753,7 +772,7 @@ __global__ void __launch_bounds__(kMaxThreads) read_kernel(CollParams p) {
         if (len) {
           const u64 coff = (u64)q * p.chunk_bytes + s * p.slice_bytes;
           const rsrc_t in = make_rsrc(p.peer_recv[q] + coff, len);
-          move<T, OPC, VEC, kCopy, kPushU>(nullptr, p.recv + coff, in, in, len, lane);
+          move<T, OPC, VEC, kCopy, kReadCopyU>(nullptr, p.recv + coff, in, in, len, lane);
         }
       }
     }
