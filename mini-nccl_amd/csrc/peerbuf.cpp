@@ -154,7 +154,7 @@ char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHa
     for (size_t i = 0; i < peers_.size(); ++i)
       if (!peers_[i].pinned && (lru == peers_.size() || peers_[i].last_use < peers_[lru].last_use)) lru = i;
     sync_previous();
-    hipIpcCloseMemHandle(peers_[lru].local);
+    (void)hipIpcCloseMemHandle(peers_[lru].local);
     peers_.erase(peers_.begin() + (long)lru);
   }
   void* p = nullptr;
@@ -169,7 +169,7 @@ char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHa
 }
 
 void PeerBuffers::close_all() {
-  for (Mapping& m : peers_) hipIpcCloseMemHandle(m.local);
+  for (Mapping& m : peers_) (void)hipIpcCloseMemHandle(m.local);
   peers_.clear();
   (void)hipGetLastError();
 }

@@ -383,8 +383,12 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
 #include <stdexcept>
 #include <string>
 
+#include <unistd.h>
+
 #include "bootstrap.h"
 #include "config.h"
+#include "kernels.h"
+#include "peerbuf.h"
 
 extern "C" {
 
@@ -406,6 +410,50 @@ int mnccl_bootstrap_selftest(int rank, int nranks, const char* ip, int port, int
     return 0;
   } catch (const std::exception& e) {
     fprintf(stderr, "bootstrap selftest rank %d: %s\n", rank, e.what());
+    return -1;
+  }
+}
+
+// The read schedule's per-call rendezvous (csrc/peerbuf.cpp) across real processes, without a
+// GPU: every call is negotiated with eligible = false (host buffers), so no HIP call is made
+// and the decision must be kFallback on every rank -- except where the ranks disagree on the
+// count (scenario 1: call calls/2 -> kMismatch everywhere) or one rank never calls (scenario 2:
+// the others time out).  Scenario 3 adds random host delays per rank (the 16-record board
+// wraps around many times).  decisions[i] = PeerBuffers::Decision of call i, -9 on timeout.
+// Returns 0, -1 on an unexpected exception, -3 without shared memory.
+int mnccl_board_selftest(int rank, int nranks, const char* ip, int port, int scenario, int calls,
+                         double timeout_s, int* decisions) {
+  try {
+    mnccl::Bootstrap b;
+    b.connect(rank, nranks, ip ? ip : "127.0.0.1", port, 20.0);
+    std::vector<uint64_t> nonces((size_t)nranks);
+    for (int q = 0; q < nranks; ++q) nonces[(size_t)q] = 1000u + (uint64_t)q;  // one process per rank
+    mnccl::PeerBuffers pb;
+    pb.init(b, rank, nranks, nonces, port);
+    if (!pb.available()) return -3;
+    uint64_t rng = 0x9E3779B97F4A7C15ull * (uint64_t)(rank + 1);
+    for (int i = 0; i < calls; ++i) decisions[i] = 99;
+    for (int i = 0; i < calls; ++i) {
+      if (scenario == 2 && rank == nranks - 1) break;  // this rank never reaches the calls
+      if (scenario == 3) {
+        rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+        usleep((useconds_t)((rng >> 33) % 300));
+      }
+      const uint64_t count = (scenario == 1 && i == calls / 2) ? 1000u + (uint64_t)rank : 1000u;
+      const char* ps[mnccl::kMaxRanks] = {};
+      const char* pr[mnccl::kMaxRanks] = {};
+      bool vec = false;
+      try {
+        decisions[i] = (int)pb.negotiate(nullptr, nullptr, false, count, 7, 0, timeout_s, [] {}, ps, pr, &vec);
+      } catch (const std::runtime_error&) {
+        decisions[i] = -9;
+        break;
+      }
+    }
+    b.barrier();
+    return 0;
+  } catch (const std::exception& e) {
+    fprintf(stderr, "board selftest rank %d: %s\n", rank, e.what());
     return -1;
   }
 }

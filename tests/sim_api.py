@@ -20,6 +20,7 @@ def load():
         vp, u64, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
         L.mnccl_sim_allreduce.argtypes = [u64, ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64, u64, i, i, i, i, i,
                                           u64, ctypes.POINTER(u64)]
+        L.mnccl_board_selftest.argtypes = [i, i, ctypes.c_char_p, i, i, i, ctypes.c_double, ctypes.POINTER(i)]
         L.mnccl_read_slice.argtypes = [u64, i, u64, u64, i]
         L.mnccl_read_slice.restype = u64
         L.mnccl_direct_phase_at.argtypes = [ctypes.c_uint32, ctypes.c_uint32, i, ctypes.POINTER(i),
@@ -88,3 +89,10 @@ def direct_phase_at(j, iters, overlap):
     ph, it = ctypes.c_int(), ctypes.c_uint32()
     load().mnccl_direct_phase_at(j, iters, overlap, ctypes.byref(ph), ctypes.byref(it))
     return ph.value, it.value
+
+
+def board_selftest(rank, nranks, port, scenario, calls, timeout_s=2.0):
+    """csrc/peerbuf.cpp's per-call rendezvous on real processes (no GPU): (rc, decisions)."""
+    dec = (ctypes.c_int * calls)()
+    rc = load().mnccl_board_selftest(rank, nranks, b"127.0.0.1", port, scenario, calls, timeout_s, dec)
+    return rc, list(dec)

@@ -60,3 +60,43 @@ def test_gloo_harness_bootstrap_and_host_ring(oracle_lib, sim_lib, world):
         assert out[r]["max"] == 10.0 + world - 1
         assert out[r]["boot"] == 0
         assert out[r]["ring_rc"] == 0 and out[r]["ring_exact"], out[r]
+
+
+def _board_rank(rank, world, port, scenario, calls, out_q):
+    try:
+        sys.path[:0] = [HERE, ROOT, os.path.join(ROOT, "mini-nccl_amd")]
+        import sim_api as S
+        t0 = time.time()
+        rc, dec = S.board_selftest(rank, world, port, scenario, calls, timeout_s=2.0)
+        out_q.put((rank, {"rc": rc, "dec": dec, "secs": time.time() - t0}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("scenario", [0, 1, 2, 3], ids=["agree", "count-mismatch", "rank-missing", "jitter"])
+def test_read_schedule_rendezvous_across_processes(sim_lib, world, scenario):
+    # csrc/peerbuf.cpp, one process per rank, no GPU: every call's records on the shared-memory
+    # board; host buffers everywhere -> the scratch fallback on every rank (PeerBuffers::kFallback
+    # = 0); a count that differs on one call -> kMismatch (-1) on every rank for that call only;
+    # a rank that never calls -> the others fail that call after the timeout (-9) instead of
+    # hanging; random per-rank delays over 64 calls (the 16-record board wraps 4 times) -> same
+    import gpu_workers as GW
+    calls = 64 if scenario == 3 else 24
+    port = GW.free_port()
+    out = GW.run_ranks(_board_rank, world, lambda r: (r, world, port, scenario, calls), 120)
+    assert sorted(out) == list(range(world)), out
+    for r in range(world):
+        assert "error" not in out[r], out[r].get("error")
+        assert out[r]["rc"] == 0, out[r]
+        dec = out[r]["dec"]
+        if scenario == 2:
+            if r == world - 1:
+                assert dec == [99] * calls  # never called
+            else:
+                assert dec[0] == -9 and out[r]["secs"] < 30, out[r]
+        else:
+            exp = [0] * calls
+            if scenario == 1:
+                exp[calls // 2] = -1
+            assert dec == exp, (r, dec)

@@ -17,7 +17,7 @@ run() {
   echo "$tag | $(tail -1 /tmp/vs_0.log) rc=$rc"
   if [ $rc -eq 124 ] || [ $rc -eq 137 ]; then exit 9; fi
 }
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for algo in $ALGOS; do
     for v in default ${VARIANTS}; do
       lib=$R/mini-nccl_amd/lib; [ $v != default ] && lib=$R/tools/variants/$v
