@@ -2,7 +2,8 @@
 // on host code only -- GPU ASan is not available on the test pool).  Built and run by
 // tests/test_host_sanitizers.py with g++ -fsanitize=address,undefined; exercises the code
 // the GPU path shares with the CPU simulator: csrc/schedule.h index math (through sim.cpp's
-// kernel-mirroring programs), the TCP bootstrap (threads over 127.0.0.1) and env config parsing.
+// kernel-mirroring programs: ring, direct and read), the TCP bootstrap (threads over 127.0.0.1),
+// the read schedule's shared-memory call board (csrc/peerbuf.cpp) and env config parsing.
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -12,11 +13,13 @@
 #include <vector>
 
 extern "C" {
-int mnccl_sim_allreduce(int algo, const float* const* send, float* const* recv, int n, uint64_t count, int op,
+int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* recv, int n, uint64_t count, int op,
                         uint64_t slice_bytes, uint64_t min_slice, int direct_overlap, int pull, int channels,
                         int slots, int calls, uint64_t schedule_seed, uint64_t* steps_out);
 int mnccl_bootstrap_selftest(int rank, int nranks, const char* ip, int port, int timeout_ms);
 int mnccl_config_describe(char* buf, int len);
+int mnccl_board_selftest(int rank, int nranks, const char* ip, int port, int scenario, int calls, double timeout_s,
+                         int* decisions);
 }
 
 static int sim_case(int algo, int n, uint64_t count, uint64_t slice, uint64_t min_slice, int overlap, int channels,
@@ -33,7 +36,8 @@ static int sim_case(int algo, int n, uint64_t count, uint64_t slice, uint64_t mi
     rp.push_back(r[(size_t)i].data());
   }
   uint64_t steps = 0;
-  const int mask = algo ? (1 << calls) - 1 : 0;
+  uint64_t mask = 0;  // 2 bits per call: the schedule of every call
+  for (int c = 0; c < calls; ++c) mask |= (uint64_t)algo << (2 * c);
   // pull placement on odd seeds: the same protocol with every slot in the sender's scratch
   const int rc = mnccl_sim_allreduce(mask, sp.data(), rp.data(), n, count, 0, slice, min_slice, overlap, (int)(seed & 1),
                                      channels, slots, calls, seed, &steps);
@@ -50,7 +54,7 @@ static int sim_case(int algo, int n, uint64_t count, uint64_t slice, uint64_t mi
 int main() {
   int fails = 0;
   const uint64_t counts[] = {7, 1000, 4099, 70001};
-  for (int algo = 0; algo < 2; ++algo)
+  for (int algo = 0; algo < 3; ++algo)
     for (int n = 2; n <= 8; n += 3)
       for (uint64_t c : counts)
         for (int overlap = 0; overlap < 2; ++overlap) {
@@ -72,6 +76,23 @@ int main() {
       printf("bootstrap FAIL rank %d rc=%d\n", r, rcs[(size_t)r]);
       ++fails;
     }
+  // the read schedule's call board: 3 ranks as threads, 40 calls with a count mismatch at call 20
+  {
+    std::vector<std::vector<int>> dec(3, std::vector<int>(40, -7));
+    std::vector<int> brc(3, -9);
+    std::vector<std::thread> bt;
+    for (int r = 0; r < 3; ++r)
+      bt.emplace_back([&, r] { brc[(size_t)r] = mnccl_board_selftest(r, 3, "127.0.0.1", port + 1, 1, 40, 10.0, dec[(size_t)r].data()); });
+    for (auto& t : bt) t.join();
+    for (int r = 0; r < 3; ++r) {
+      bool ok = brc[(size_t)r] == 0;
+      for (int i = 0; i < 40; ++i) ok = ok && dec[(size_t)r][(size_t)i] == (i == 20 ? -1 : 0);
+      if (!ok) {
+        printf("board FAIL rank %d rc=%d\n", r, brc[(size_t)r]);
+        ++fails;
+      }
+    }
+  }
   char buf[512];
   if (mnccl_config_describe(buf, (int)sizeof buf) != 0) {
     printf("config FAIL: %s\n", buf);

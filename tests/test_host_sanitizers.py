@@ -20,9 +20,10 @@ def test_host_logic_under_asan_ubsan(tmp_path):
     import gpu_workers as GW
     exe = str(tmp_path / "host_selftest")
     srcs = [os.path.join(ROOT, "tests", "native", "host_selftest.cpp")] + \
-        [os.path.join(CSRC, f) for f in ("sim.cpp", "bootstrap.cpp", "config.cpp")]
+        [os.path.join(CSRC, f) for f in ("sim.cpp", "bootstrap.cpp", "config.cpp", "peerbuf.cpp")]
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
-           "-fno-sanitize-recover=undefined", "-pthread", "-I" + CSRC, "-o", exe] + srcs
+           "-fno-sanitize-recover=undefined", "-pthread", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+           "-I" + CSRC, "-o", exe] + srcs + ["-L/opt/rocm/lib", "-lamdhip64", "-lrt", "-Wl,-rpath,/opt/rocm/lib"]
     subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300)
     env = dict(os.environ, SELFTEST_PORT=str(GW.free_port()), ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
                UBSAN_OPTIONS="print_stacktrace=1")
