@@ -39,8 +39,11 @@ COUNT = 268435456  # 1 GiB of fp32
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+_T0 = time.time()
+
+
 def log(*a):
-    print(*a, file=sys.stderr, flush=True)
+    print(f"[{time.time() - _T0:7.1f}s]", *a, file=sys.stderr, flush=True)
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle)
@@ -187,7 +190,7 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
         torch.cuda.synchronize()
         dt = max_over_ranks(time.perf_counter() - t0)
         ok = comm.async_error() == 0 and bool((recv == float(n)).all().item())
-        ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, st, 1)
+        ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, st, 1, dist.barrier)
         i = comm.info()
         ok = ok and i["last_algo"] == ALGO_NAMES.index(algo)  # the point ran its own schedule
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
@@ -206,7 +209,7 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
         torch.cuda.empty_cache()
 
 
-def verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream, calls=3):
+def verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream, calls=3, barrier=None):
     """Cross-rank result check that a protocol race cannot pass: every call gets new,
     rank- and position-dependent integer-valued inputs (sums exact in any order and in
     bf16/f16), so a stale or torn slot, a missed hand-off or a wrong chunk owner shows up
@@ -214,39 +217,64 @@ def verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stre
     mod = 1021 if tdt == torch.float32 else 8
     chunk = count // n
     body = chunk * n
-    ok = True
+    piece = 1 << 26  # inputs and expected values built 64 Mi elements at a time: a 4 GiB C4 point
+    ok = True        # needs no temporaries beyond send / recv (8 ranks may share one GPU's HBM)
+
+    def vals(a, b, q, c):
+        return (torch.arange(a, b, device=dev, dtype=torch.int64) + (7 * q + 31 * c)) % mod
+
     for c in range(calls):
-        idx = torch.arange(count, device=dev, dtype=torch.int64)
-        send.copy_(((idx + 7 * rank + 31 * c) % mod).to(tdt))
-        exp = torch.zeros(count, device=dev, dtype=torch.float32)
-        for q in range(n):
-            exp += ((idx + 7 * q + 31 * c) % mod).to(torch.float32)
-        exp[body:] = send[body:].float()  # the count % n tail keeps this rank's input
-        del idx
+        for a in range(0, count, piece):
+            b = min(count, a + piece)
+            send[a:b].copy_(vals(a, b, rank, c))
         recv.fill_(-1)
         torch.cuda.synchronize()
+        if barrier is not None:
+            barrier()  # every rank enters the call together: input preparation is not the call's skew
         rc = comm.all_reduce(send.data_ptr(), recv.data_ptr(), count, ndt, M.ncclSum, stream.cuda_stream)
         torch.cuda.synchronize()
-        ok = ok and rc == 0 and comm.async_error() == 0 and bool(torch.equal(recv.float(), exp))
-        del exp
+        ok = ok and rc == 0 and comm.async_error() == 0
+        for a in range(0, count, piece):
+            if not ok:
+                break
+            b = min(count, a + piece)
+            exp = torch.zeros(b - a, device=dev, dtype=torch.float32)
+            for q in range(n):
+                exp += vals(a, b, q, c).to(torch.float32)
+            if b > body:  # the count % n tail keeps this rank's input
+                exp[max(body, a) - a:] = send[max(body, a):b].float()
+            ok = bool(torch.equal(recv[a:b].float(), exp))
+            del exp
     return ok
 
 
-def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
-    out = {"buffer": "256 MiB fp32", "points": []}
-    for i, (algo, env) in enumerate(SWEEP_POINTS):
-        if rank == 0:
-            log(f"sweep {i + 1}/{len(SWEEP_POINTS)}: {algo} {env}")
-        r = sweep_point(M, torch, dist, dev, n, rank, env, algo, 64 << 20, 5, max_over_ranks)
-        out["points"].append({"algo": algo, "env": {k[len("MINI_NCCL_"):].lower(): v for k, v in env.items()}, **r})
-    if with_c4:  # BASELINE.json configs[3]: ring, 4 GiB fp32, SLICE x WINDOW
+def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_point=lambda: None):
+    """fills `out` point by point (on_point after each), so a guard that ends the run early or a
+    crash still reports what ran.  BASELINE.json's own configs go first (C5, then the C4 grid),
+    the exploratory (schedule, knob) points on 256 MiB after them."""
+    if with_c4:
+        # BASELINE.json configs[4] (C5): 1 GiB of bf16 / fp16 per rank, library defaults; the
+        # check is exact (integer-valued sums stay exact in 2-byte floats)
+        c5 = out["c5_read_1GiB"] = {}
+        for dt in ("bf16", "f16"):
+            if rank == 0:
+                log(f"C5: read {dt}")
+            c5[dt] = sweep_point(M, torch, dist, dev, n, rank, {}, "read", (1 << 30) // 2, 5, max_over_ranks, dtype=dt)
+            on_point()
+        # BASELINE.json configs[3] (C4): ring, 4 GiB fp32, SLICE x WINDOW
         out["c4_buffer_MiB"] = C4_COUNT * 4 >> 20
         out["c4_knobs"] = ("SLICE_SIZE = payload bytes per message; WINDOW_SIZE x SIGNAL_BATCH (16) = messages in "
                            "flight per link, the reference's bound (mini_nccl.cu:119,144,167): pipelines x 2 slots <= "
                            "WINDOW x 16, at most 256 pipelines; scratch capped at MINI_NCCL_SCRATCH_MB (512): "
                            "(n-1) x pipelines x 2 x SLICE <= cap, so large slices run fewer pipelines "
                            "(csrc/schedule.h pipeline_geometry; each point reports its geometry)")
-        c4 = []
+        # the same 4 GiB with the library defaults (the read schedule) and with the direct one
+        for key, algo in (("c4_read_4GiB_defaults", "read"), ("c4_direct_4GiB_defaults", "direct")):
+            if rank == 0:
+                log(f"C4: {algo} defaults")
+            out[key] = sweep_point(M, torch, dist, dev, n, rank, {}, algo, C4_COUNT, 3, max_over_ranks)
+            on_point()
+        c4 = out["c4_ring_4GiB"] = []
         for w in C4_WINDOWS:
             for sl in C4_SLICES:
                 env = {"MINI_NCCL_WINDOW_SIZE": w, "MINI_NCCL_SLICE_SIZE": sl}
@@ -254,16 +282,14 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4):
                     log(f"C4: ring {env}")
                 r = sweep_point(M, torch, dist, dev, n, rank, env, "ring", C4_COUNT, 3, max_over_ranks)
                 c4.append({"window": w, "slice": sl, **r})
-        out["c4_ring_4GiB"] = c4
-        # the same 4 GiB with the library defaults (the read schedule) and with the direct one
-        out["c4_read_4GiB_defaults"] = sweep_point(M, torch, dist, dev, n, rank, {}, "read", C4_COUNT, 3,
-                                                   max_over_ranks)
-        out["c4_direct_4GiB_defaults"] = sweep_point(M, torch, dist, dev, n, rank, {}, "direct", C4_COUNT, 3,
-                                                     max_over_ranks)
-        # BASELINE.json configs[4] (C5): 1 GiB of bf16 / fp16 per rank, library defaults; the
-        # check is exact (integer-valued sums stay exact in 2-byte floats)
-        out["c5_read_1GiB"] = {dt: sweep_point(M, torch, dist, dev, n, rank, {}, "read", (1 << 30) // 2, 5,
-                                               max_over_ranks, dtype=dt) for dt in ("bf16", "f16")}
+                on_point()
+    out.update({"buffer": "256 MiB fp32", "points": []})
+    for i, (algo, env) in enumerate(SWEEP_POINTS):
+        if rank == 0:
+            log(f"sweep {i + 1}/{len(SWEEP_POINTS)}: {algo} {env}")
+        r = sweep_point(M, torch, dist, dev, n, rank, env, algo, 64 << 20, 5, max_over_ranks)
+        out["points"].append({"algo": algo, "env": {k[len("MINI_NCCL_"):].lower(): v for k, v in env.items()}, **r})
+        on_point()
     return out
 
 
@@ -501,7 +527,15 @@ def emit(result):
         if _crash and _crash[0] is not None:
             _crash[0].crashline_disarm()
         sys.stdout.flush()
-        os.write(_json_fd[0], (json.dumps(result) + "\n").encode())
+        for attempt in range(5):  # the guard thread may serialise while the main thread adds a point
+            try:
+                line = json.dumps(result)
+                break
+            except RuntimeError:
+                time.sleep(0.05)
+        else:
+            line = json.dumps({k: v for k, v in list(result.items()) if k != "sweep"})
+        os.write(_json_fd[0], (line + "\n").encode())
 
 
 def main():
@@ -671,7 +705,8 @@ def main():
             ae = comm.async_error()
             ok = ok and ae == 0 and bool((recv == float(n)).all().item())
             # then 3 calls on varying data (outside the timed region), restoring the buffers
-            ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream)
+            ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream,
+                                    barrier=dist.barrier)
             ok = ok and comm.info()["last_algo"] == ALGO_NAMES.index(algo)  # no fallback happened
             send.fill_(1.0)
             ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
@@ -829,7 +864,8 @@ def main():
         import threading
 
         def bail():
-            result["extras"] = f"RCCL reference / sweeps unfinished after {EXTRAS_LIMIT_S} s: skipped"
+            result["extras"] = (f"RCCL reference / sweeps unfinished after {EXTRAS_LIMIT_S} s: the rest skipped "
+                                "(the points above ran)")
             if rank == 0:
                 emit(result)
             os._exit(0)
@@ -890,7 +926,10 @@ def main():
         torch.cuda.empty_cache()
         if not args.no_sweep and args.dtype == "f32":
             t_sw = time.time()
-            result["sweep"] = run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4=(n == 8 or os.environ.get("MNCCL_BENCH_C4") == "1"))
+            result["sweep"] = {}
+            run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks,
+                       with_c4=(n == 8 or os.environ.get("MNCCL_BENCH_C4") == "1"), out=result["sweep"],
+                       on_point=(lambda: arm(result)) if rank == 0 else (lambda: None))
             result["sweep"]["wall_s"] = round(time.time() - t_sw, 1)
     if guard is not None:
         guard.cancel()

@@ -641,6 +641,7 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
       } catch (const std::exception& e) {
         fprintf(stderr, "[Mini-NCCL] rank %d: %s; communicator is no longer usable\n", rank_, e.what());
         sticky_ = ncclInternalError;
+        abort_peers();
         if (cur_dev != device_) hipSetDevice(cur_dev);
         return sticky_;
       }
@@ -668,6 +669,21 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
   if (cur_dev != device_) hipSetDevice(cur_dev);
   if (cfg_.blocking && cap == hipStreamCaptureStatusNone) return wait_for(stream, seq);
   return ncclSuccess;
+}
+
+void Comm::abort_peers() {
+  static const uint64_t one = 1;
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  const uint64_t w = mbox_abort(nranks_, wave_channels());
+  for (int q = 0; q < nranks_; ++q)
+    if (q != rank_ && peer_mbox_[(size_t)q]) (void)hipMemcpyAsync(peer_mbox_[(size_t)q] + w, &one, sizeof one, hipMemcpyHostToDevice, st);
+  (void)hipStreamSynchronize(st);
+  (void)hipStreamDestroy(st);
+  (void)hipGetLastError();
 }
 
 ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gbps) {

@@ -68,6 +68,10 @@ class Comm {
   bool device_local(const void* p) const;  // device memory of this rank's GPU (not managed)
   void wait_previous_call();
   ncclResult_t check_status();
+  // a rank that gives up on a call outside its kernel (the read schedule's rendezvous) raises
+  // every peer's ABORT word, as a timed-out kernel does, so the peers fail fast instead of
+  // running into their own watchdog
+  void abort_peers();
 
   int rank_, nranks_, device_ = 0;
   Config cfg_;

@@ -392,8 +392,16 @@ def stall_rank(rank, n, port, env, call_allreduce, out_q):
             res["secs"] = time.time() - t0
             res["rc2"] = comm.all_reduce(buf.ptr, buf.ptr, (1 << 20) // 4, M.ncclFloat, M.ncclSum, 0)
             res["async"] = comm.async_error()
+            if env.get("LATE_CALL") == "1":  # keep the buffer and the memory alive for the late rank
+                time.sleep(max(0.0, float(env.get("STALL_SECS", "4")) + 4.0 - (time.time() - t0)))
         else:
             time.sleep(float(env.get("STALL_SECS", "4")))
+            if env.get("LATE_CALL") == "1":
+                # arrives after rank 0 gave up: rank 0 raised this rank's ABORT word, so the
+                # kernel fails at once (ncclRemoteError) instead of waiting out its watchdog
+                t0 = time.time()
+                res["rc"] = comm.all_reduce(buf.ptr, buf.ptr, (1 << 20) // 4, M.ncclFloat, M.ncclSum, 0)
+                res["secs"] = time.time() - t0
         out_q.put((rank, res))
         buf.free()
         comm.destroy()

@@ -290,6 +290,20 @@ def test_watchdog_timeout_is_internal_error_and_sticky(dev):
     assert out[0]["async"] == M.ncclInternalError
 
 
+@pytest.mark.parametrize("algo", ["ring", "read"])
+def test_late_peer_is_aborted_fast(dev, algo):
+    # rank 0 gives up on rank 1 (kernel watchdog for ring, the read schedule's rendezvous limit
+    # for read); either way it raises rank 1's ABORT word, so rank 1's late call fails at once
+    import mini_nccl as M
+    port = GW.free_port()
+    env = {"MINI_NCCL_TIMEOUT_MS": "1500", "STALL_SECS": "7", "LATE_CALL": "1", "MINI_NCCL_ALGO": algo}
+    out = GW.run_ranks(GW.stall_rank, 2, lambda r: (r, 2, port, env, r == 0), 120)
+    assert sorted(out) == [0, 1] and all("error" not in v for v in out.values()), out
+    assert out[0]["rc"] == M.ncclInternalError and out[0]["secs"] < 15
+    assert out[1]["rc"] == M.ncclRemoteError, out[1]
+    assert out[1]["secs"] < 1.5, out[1]  # well under its own 1.5 s watchdog + 2 s host limit
+
+
 @pytest.mark.parametrize("algo", ["ring", "direct", "read"])
 def test_allreduce_hip_graph_capture_and_replay(dev, algo):
     # the reference only warns under capture (api.cpp:153-166); here a captured all-reduce
