@@ -132,6 +132,79 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def fullsize_input(rank, count, dtype, seed=1234, piece=1 << 24):
+    """Rank r's full-size buffer: seeded uniform[-1, 1) (seed = 1234 + r),
+    generated piece by piece (the same stream as one call) so no float64 temporary of the whole
+    buffer is needed.  The parent and the rank process build identical bytes independently."""
+    import oracle_api as O
+    code, npd = O.DTYPES[dtype]
+    g = np.random.default_rng(seed + rank)
+    out = np.empty(count, dtype=npd)
+    f = np.empty(min(piece, count), dtype=np.float32)
+    for a in range(0, count, piece):
+        b = min(count, a + piece)
+        v = f[:b - a]
+        g.random(dtype=np.float32, out=v)  # [0, 1)
+        v *= 2
+        v -= 1
+        if dtype == "bf16":  # truncated to bf16 (the top 16 bits: exact, no rounding step)
+            out[a:b] = v.view(np.uint32) >> 16
+        else:
+            out[a:b] = v
+    return out
+
+
+def block_digests(arr, block_bytes=1 << 24):
+    """sha1 of every 16 MiB block: a full-size result is compared by digest, and a mismatch is
+    located to its block without shipping the buffer between processes."""
+    import hashlib
+    mv = memoryview(np.ascontiguousarray(arr).view(np.uint8))
+    return [hashlib.sha1(mv[i:i + block_bytes]).hexdigest() for i in range(0, len(mv), block_bytes)]
+
+
+def fullsize_rank(rank, n, port, env, dtype, count, algos, out_q, barrier=None):
+    """One full-size all-reduce per schedule in `algos` (BASELINE C3 / C5 sizes) on this rank's
+    seeded input, in place and out of place alternately; reports the block digests of recv."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        hip_rt.set_device(0)
+        x = fullsize_input(rank, count, dtype)
+        code, npd = O.DTYPES[dtype]
+        comm = M.Comm(n, rank, "127.0.0.1")
+        stream = hip_rt.Stream()
+        send = hip_rt.DeviceBuffer(x.nbytes)
+        recv = hip_rt.DeviceBuffer(x.nbytes)
+        res = []
+        for i, algo in enumerate(algos):
+            inplace = i % 2 == 1
+            comm.set_algo(algo)
+            send.upload(x)
+            dst = send if inplace else recv
+            if not inplace:
+                recv.fill_byte(0xAB)
+            stream.sync()
+            if barrier is not None:
+                barrier.wait(300)
+            t0 = time.time()
+            rc = comm.all_reduce(send.ptr, dst.ptr, count, code, M.ncclSum, stream.handle)
+            stream.sync()
+            secs = time.time() - t0
+            got = dst.download(npd, count)
+            res.append({"algo": algo, "inplace": inplace, "rc": rc, "async": comm.async_error(), "secs": secs,
+                        "last_algo": comm.info()["last_algo"], "digests": block_digests(got)})
+            del got
+        send.free()
+        recv.free()
+        stream.destroy()
+        out_q.put((rank, {"results": res, "destroy": comm.destroy()}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
 def graph_rank(rank, n, port, env, replays, out_q):
     """Capture one ncclAllReduce into a HIP graph, replay it `replays` times with fresh input
     each time; the per-pair sequence counters live on the device, so replays stay in step."""

@@ -90,6 +90,37 @@ def ring_fold(inputs, dtype="f32", op="sum"):
     return out
 
 
+def ring_fold_parallel(inputs, dtype="f32", op="sum", threads=8, piece=1 << 22):
+    """ring_fold for full-size buffers: the same closed form (chunk c starts from x[c], then
+    acc = op(x[q], acc) for q = c+1, ..., c-1, mini_nccl.cu:108-194), each chunk cut into pieces
+    folded by oracle_reduce on a thread pool (ctypes releases the GIL; element-wise work, so the
+    bits are ring_fold's).  The count % n tail is rank 0's input, as in ring_fold."""
+    from concurrent.futures import ThreadPoolExecutor
+    code, npd = DTYPES[dtype]
+    n = len(inputs)
+    ins = [np.ascontiguousarray(x, dtype=npd) for x in inputs]
+    count = ins[0].size
+    chunk = count // n
+    out = np.empty_like(ins[0])
+    out[n * chunk:] = ins[0][n * chunk:]
+    L = load()
+
+    def job(c, a, b):
+        lo, hi = c * chunk + a, c * chunk + b
+        acc = out[lo:hi]
+        acc[:] = ins[c][lo:hi]
+        for k in range(1, n):
+            src = ins[(c + k) % n][lo:hi]
+            if L.oracle_reduce(_ptr(acc), _ptr(src), _ptr(acc), hi - lo, code, OPS[op]) != 0:
+                raise ValueError("oracle_reduce rejected arguments")
+
+    with ThreadPoolExecutor(threads) as ex:
+        futs = [ex.submit(job, c, a, min(chunk, a + piece)) for c in range(n) for a in range(0, chunk, piece)]
+        for f in futs:
+            f.result()
+    return out
+
+
 def reduce(a, b, dtype="f32", op="sum"):
     """Element-wise c = op(a = local, b = incoming) (mini_nccl.cu:43-47)."""
     code, npd = DTYPES[dtype]

@@ -234,6 +234,36 @@ def test_read_schedule_allocation_churn(dev):
         assert out[r]["results"][-1]["peer_mappings"] >= 2
 
 
+@pytest.mark.parametrize("dtype,algos", [("f32", (2, 0)), ("bf16", (2,)), ("f16", (2,))],
+                         ids=["c3_f32_read_ring", "c5_bf16_read", "c5_f16_read"])
+def test_allreduce_8_ranks_full_size(dev, dtype, algos):
+    # BASELINE C3 (8 ranks, 1 GiB fp32; the read default and the reference's ring) and C5
+    # (8 ranks, 1 GiB fp16 / bf16) at their FULL sizes, seeded uniform[-1, 1) inputs (order-
+    # sensitive), bit-exact against the oracle's closed-form ring fold -- itself pinned to the
+    # loop-by-loop restatement of mini_nccl.cu:108-194 (tests/test_oracle.py).  The ranks
+    # report 16 MiB block digests of their result; the oracle's digests are computed here.
+    n = 8
+    count = (1 << 30) // (4 if dtype == "f32" else 2)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(n) as ex:
+        xs = list(ex.map(lambda r: GW.fullsize_input(r, count, dtype), range(n)))
+    exp = GW.block_digests(O.ring_fold_parallel(xs, dtype, "sum"))
+    del xs
+    port = GW.free_port()
+    env = {"MINI_NCCL_TIMEOUT_MS": "60000", "MINI_NCCL_TUNE": "0"}
+    out = GW.run_ranks(GW.fullsize_rank, n, lambda r: (r, n, port, env, dtype, count, algos), 600, barrier=True)
+    assert sorted(out) == list(range(n)), f"only ranks {sorted(out)} reported"
+    for r in range(n):
+        assert "error" not in out[r], f"rank {r}:\n{out[r]['error']}"
+        assert out[r]["destroy"] == 0
+        for res in out[r]["results"]:
+            assert res["rc"] == 0 and res["async"] == 0, (r, res["algo"], res["rc"], res["async"])
+            assert res["last_algo"] == res["algo"], (r, res["algo"], res["last_algo"])
+            bad = [i for i, (g, e) in enumerate(zip(res["digests"], exp)) if g != e]
+            assert len(res["digests"]) == len(exp) and not bad, \
+                f"rank {r} schedule {res['algo']} in_place={res['inplace']}: 16 MiB blocks {bad[:8]} differ"
+
+
 def test_allreduce_c2_full_size(dev):
     # BASELINE.json configs[1] (C2): 2 ranks, 256 MiB fp32, MINI_NCCL_SLICE_SIZE = 128 KiB,
     # seeded uniform inputs, bit-exact against the oracle at full size

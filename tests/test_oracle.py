@@ -109,3 +109,13 @@ def test_verify_scan_finds_first_mismatch(oracle_lib):
     x[517] = 4.0
     x[1000] = 0.0  # scalar tail (perf_test.cpp:128-134)
     assert L.oracle_verify_avx2(x.ctypes.data, x.size, 4.0) == 1000
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16", "bf16", "i32"])
+@pytest.mark.parametrize("count", [8 * 4099, 8 * 4099 + 5])
+def test_ring_fold_parallel_matches_ring_fold(dtype, count):
+    # the threaded closed-form fold the full-size GPU tests compare against gives ring_fold's bits
+    xs = O.random_inputs(8, count, dtype, seed=77)
+    a = O.ring_fold(xs, dtype, "sum")
+    b = O.ring_fold_parallel(xs, dtype, "sum", piece=1000)
+    assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
