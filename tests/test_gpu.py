@@ -234,23 +234,29 @@ def test_read_schedule_allocation_churn(dev):
         assert out[r]["results"][-1]["peer_mappings"] >= 2
 
 
-@pytest.mark.parametrize("dtype,algos", [("f32", (2, 0)), ("bf16", (2,)), ("f16", (2,))],
-                         ids=["c3_f32_read_ring", "c5_bf16_read", "c5_f16_read"])
-def test_allreduce_8_ranks_full_size(dev, dtype, algos):
-    # BASELINE C3 (8 ranks, 1 GiB fp32; the read default and the reference's ring) and C5
-    # (8 ranks, 1 GiB fp16 / bf16) at their FULL sizes, seeded uniform[-1, 1) inputs (order-
-    # sensitive), bit-exact against the oracle's closed-form ring fold -- itself pinned to the
-    # loop-by-loop restatement of mini_nccl.cu:108-194 (tests/test_oracle.py).  The ranks
-    # report 16 MiB block digests of their result; the oracle's digests are computed here.
+@pytest.mark.parametrize("dtype,algos,gib,knobs", [
+    ("f32", (2, 0), 1, {}), ("bf16", (2,), 1, {}), ("f16", (2,), 1, {}),
+    # C4: 4 GiB fp32, the grid's extreme geometries (WINDOW 16 -> 128 pipelines with 64 KiB
+    # slices; 1 MiB slices -> 36 pipelines under the scratch cap), ring as C4 names it
+    ("f32", (0, 2), 4, {"MINI_NCCL_SLICE_SIZE": "65536", "MINI_NCCL_WINDOW_SIZE": "16"}),
+    ("f32", (0,), 4, {"MINI_NCCL_SLICE_SIZE": "1048576", "MINI_NCCL_WINDOW_SIZE": "64"})],
+    ids=["c3_f32_read_ring", "c5_bf16_read", "c5_f16_read", "c4_64k_w16_ring_read", "c4_1m_w64_ring"])
+def test_allreduce_8_ranks_full_size(dev, dtype, algos, gib, knobs):
+    # BASELINE C3 (8 ranks, 1 GiB fp32; the read default and the reference's ring), C5
+    # (8 ranks, 1 GiB fp16 / bf16) and C4 (8 ranks, 4 GiB fp32) at their FULL sizes, seeded
+    # uniform[-1, 1) inputs (order-sensitive), bit-exact against the oracle's closed-form ring
+    # fold -- itself pinned to the loop-by-loop restatement of mini_nccl.cu:108-194
+    # (tests/test_oracle.py).  The ranks report 16 MiB block digests of their result; the
+    # oracle's digests are computed here.
     n = 8
-    count = (1 << 30) // (4 if dtype == "f32" else 2)
+    count = (gib << 30) // (4 if dtype == "f32" else 2)
     from concurrent.futures import ThreadPoolExecutor
     with ThreadPoolExecutor(n) as ex:
         xs = list(ex.map(lambda r: GW.fullsize_input(r, count, dtype), range(n)))
     exp = GW.block_digests(O.ring_fold_parallel(xs, dtype, "sum"))
     del xs
     port = GW.free_port()
-    env = {"MINI_NCCL_TIMEOUT_MS": "60000", "MINI_NCCL_TUNE": "0"}
+    env = {"MINI_NCCL_TIMEOUT_MS": "60000", "MINI_NCCL_TUNE": "0", "GPU_MAX_HW_QUEUES": "2", **knobs}
     out = GW.run_ranks(GW.fullsize_rank, n, lambda r: (r, n, port, env, dtype, count, algos), 600, barrier=True)
     assert sorted(out) == list(range(n)), f"only ranks {sorted(out)} reported"
     for r in range(n):
