@@ -120,6 +120,16 @@ __device__ __forceinline__ v4u ld_slot16(rsrc_t r, uint32_t off) {
 __device__ __forceinline__ void st_slot16(rsrc_t r, uint32_t off, v4u v) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSys);
 }
+// non-temporal buffer access (this rank's own bytes in the read kernel's short-slice forms:
+// out-of-range lanes of a buffer access read 0 and write nothing, so those loops need no
+// per-lane predicate)
+constexpr int kAuxNt = 2;
+__device__ __forceinline__ v4u ld_nt16(rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxNt);
+}
+__device__ __forceinline__ void st_nt16(rsrc_t r, uint32_t off, v4u v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxNt);
+}
 // this rank's own send / recv bytes are touched once per call: non-temporal (see local reduce)
 __device__ __forceinline__ v4u ld_g16(const char* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
@@ -672,6 +682,75 @@ __device__ __forceinline__ void read_fold_scalar(const CollParams& p, uint64_t c
 #endif
 constexpr int kReadFoldU = MNCCL_READ_FOLD_U, kReadCopyU = MNCCL_READ_COPY_U;
 
+// Short slices (below one full batch, and the part of a slice past its full batches): every
+// peer's vectors of a step are loaded at once -- (n-1) x kWideV KiB in flight per wave -- so a
+// step costs one load round trip, where a peer-by-peer loop of single vectors cost one per peer
+// and vector (a 1 KiB slice over 7 peers: 1 round trip instead of 7 in the fold, and in the
+// copy).  The buffer resources end at the slice's last whole vector: lanes past it load 0 and
+// store nothing (no predicate, so no load waits on another); the last nbytes % 16 bytes go
+// element by element as before.
+constexpr int kWideV = 2;
+constexpr int kWideG = 7;  // peers per group (a node's n - 1): their buffer descriptors stay in SGPRs
+
+template <typename T, int OPC>
+__device__ __forceinline__ void read_fold_wide(const CollParams& p, uint64_t coff, uint32_t vlo, uint32_t nvec,
+                                               int lane) {
+  const int n = p.n, r = p.rank;
+  const uint32_t vb = nvec * 16;
+  const rsrc_t loc = make_rsrc(p.send + coff, vb), out = make_rsrc(p.recv + coff, vb);
+  for (uint32_t b = vlo; b < nvec; b += 64 * kWideV) {
+    v4u acc[kWideV];
+#pragma unroll
+    for (int u = 0; u < kWideV; ++u) acc[u] = ld_nt16(loc, (b + (uint32_t)(u * 64 + lane)) * 16);
+    for (int k0 = 1; k0 < n; k0 += kWideG) {  // ring order: groups in turn, peers in turn
+      v4u x[kWideG][kWideV];
+#pragma unroll
+      for (int g = 0; g < kWideG; ++g)
+        if (k0 + g < n) {
+          const rsrc_t in = make_rsrc(p.peer_send[direct_peer(n, r, k0 + g)] + coff, vb);
+#pragma unroll
+          for (int u = 0; u < kWideV; ++u) x[g][u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
+        }
+#pragma unroll
+      for (int g = 0; g < kWideG; ++g)
+        if (k0 + g < n) {
+#pragma unroll
+          for (int u = 0; u < kWideV; ++u) acc[u] = reduce16<T, OPC>(x[g][u], acc[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kWideV; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
+  }
+}
+
+// vectors [vlo, nvec) of every peer's result slice at byte soff of its chunk, into my recv
+__device__ __forceinline__ void read_copy_wide(const CollParams& p, uint64_t soff, uint32_t vlo, uint32_t nvec,
+                                               int lane) {
+  const int n = p.n, r = p.rank;
+  const uint32_t vb = nvec * 16;
+  for (uint32_t b = vlo; b < nvec; b += 64 * kWideV) {
+    for (int k0 = 1; k0 < n; k0 += kWideG) {
+      v4u y[kWideG][kWideV];
+#pragma unroll
+      for (int g = 0; g < kWideG; ++g)
+        if (k0 + g < n) {
+          const int q = direct_peer(n, r, k0 + g);
+          const rsrc_t in = make_rsrc(p.peer_recv[q] + (u64)q * p.chunk_bytes + soff, vb);
+#pragma unroll
+          for (int u = 0; u < kWideV; ++u) y[g][u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
+        }
+#pragma unroll
+      for (int g = 0; g < kWideG; ++g)
+        if (k0 + g < n) {
+          const int q = direct_peer(n, r, k0 + g);
+          const rsrc_t dst = make_rsrc(p.recv + (u64)q * p.chunk_bytes + soff, vb);
+#pragma unroll
+          for (int u = 0; u < kWideV; ++u) st_nt16(dst, (b + (uint32_t)(u * 64 + lane)) * 16, y[g][u]);
+        }
+    }
+  }
+}
+
 template <typename T, int OPC, bool VEC>
 __device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, uint32_t nbytes, int lane) {
   if (!VEC) {
@@ -708,14 +787,7 @@ __device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, ui
 #pragma unroll
     for (int u = 0; u < U; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
   }
-  for (uint32_t i = b + (uint32_t)lane; i < nvec; i += 64) {
-    v4u acc = ld_g16(lsrc + (size_t)i * 16);
-    for (int k = 1; k < n; ++k) {
-      const rsrc_t in = make_rsrc(p.peer_send[direct_peer(n, r, k)] + coff, nbytes);
-      acc = reduce16<T, OPC>(ld_slot16(in, i * 16), acc);
-    }
-    st_slot16(out, i * 16, acc);
-  }
+  if (b < nvec) read_fold_wide<T, OPC>(p, coff, b, nvec, lane);
   if (nbytes & 15u) read_fold_scalar<T, OPC>(p, coff, nbytes, lane, nvec * 16);
 }
 
@@ -762,19 +834,34 @@ __global__ void __launch_bounds__(kMaxThreads) read_kernel(CollParams p) {
     if (j > 0) {
       // G(j-1): every peer's result slice j-1, peer by peer (pipeline w starts at peer w mod
       // n-1, so a rank's pipelines spread over all links), into my recv
+      // (full batches peer by peer; the rest of the slice -- all of a short one -- for every
+      // peer at once, once all their READYs are in)
       const uint32_t t = j - 1;
       const u64 s = (u64)t * C + w;
       const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
+      const uint32_t nvec = len >> 4;
+      const uint32_t full = VEC ? nvec / (64u * kReadCopyU) * (64u * kReadCopyU) : 0;
       for (int k = 1; k < n; ++k) {
         const int q = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));
         if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx[q] + 2 + t, ctl, lane)) goto aborted;
         acquire_sys(p.sys_fence);
-        if (len) {
-          const u64 coff = (u64)q * p.chunk_bytes + s * p.slice_bytes;
+        const u64 coff = (u64)q * p.chunk_bytes + s * p.slice_bytes;
+        if (VEC && full) {
+          const rsrc_t in = make_rsrc(p.peer_recv[q] + coff, full * 16);
+          move<T, OPC, true, kCopy, kReadCopyU>(nullptr, p.recv + coff, in, in, full * 16, lane);
+        } else if (!VEC && len) {
           const rsrc_t in = make_rsrc(p.peer_recv[q] + coff, len);
-          move<T, OPC, VEC, kCopy, kReadCopyU>(nullptr, p.recv + coff, in, in, len, lane);
+          move<T, OPC, false, kCopy>(nullptr, p.recv + coff, in, in, len, lane);
         }
       }
+      if (VEC && full < nvec) read_copy_wide(p, s * p.slice_bytes, full, nvec, lane);
+      if (VEC && (len & 15u))
+        for (int k = 1; k < n; ++k) {
+          const int q = direct_peer(n, r, k);
+          const u64 coff = (u64)q * p.chunk_bytes + s * p.slice_bytes;
+          const rsrc_t in = make_rsrc(p.peer_recv[q] + coff, len);
+          move_scalar<T, OPC, kCopy>(nullptr, p.recv + coff, in, in, len, lane, nvec * 16);
+        }
     }
   }
   // DONE: every load of a peer's buffer has returned; then wait until nobody reads mine
