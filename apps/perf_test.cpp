@@ -68,21 +68,25 @@ static long first_mismatch(const float* p, size_t n, float expected) {
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "Usage: %s <rank> <n_ranks> [master_ip] [--mode device|host|staged] [--sizes 1,16,64,128]\n", argv[0]);
+    fprintf(stderr, "Usage: %s <rank> <n_ranks> [master_ip] [--mode device|host|staged] [--sizes 1,16,64,128 (MiB; 64k = KiB)]\n", argv[0]);
     return 1;
   }
   const int rank = atoi(argv[1]);
   const int nranks = atoi(argv[2]);
   const char* ip = "127.0.0.1";
   std::string mode = "device";
-  std::vector<size_t> sizes_mib = {1, 16, 64, 128};
+  std::vector<size_t> sizes = {1u << 20, 16u << 20, 64u << 20, 128u << 20};  // bytes
   int iters = 20, warmup = 5;
   for (int a = 3; a < argc; ++a) {
     std::string s = argv[a];
     if (s == "--mode" && a + 1 < argc) mode = argv[++a];
     else if (s == "--sizes" && a + 1 < argc) {
-      sizes_mib.clear();
-      for (char* t = strtok(argv[++a], ","); t; t = strtok(nullptr, ",")) sizes_mib.push_back(strtoul(t, nullptr, 10));
+      sizes.clear();  // MiB, or KiB with a "k" suffix ("4k,64k,1")
+      for (char* t = strtok(argv[++a], ","); t; t = strtok(nullptr, ",")) {
+        char* end = nullptr;
+        const size_t v = strtoul(t, &end, 10);
+        sizes.push_back(end && (*end == 'k' || *end == 'K') ? v << 10 : v << 20);
+      }
     } else if (s == "--iters" && a + 1 < argc) iters = atoi(argv[++a]);
     else if (s == "--warmup" && a + 1 < argc) warmup = atoi(argv[++a]);
     else ip = argv[a];
@@ -103,8 +107,8 @@ int main(int argc, char** argv) {
     printf("%15s %15s %15s %15s\n", "Size(B)", "Time(us)", "AlgBW(GB/s)", "BusBW(GB/s)");
   }
   int failures = 0;
-  for (size_t mib : sizes_mib) {
-    const size_t bytes = mib << 20, count = bytes / sizeof(float);
+  for (size_t bytes : sizes) {
+    const size_t count = bytes / sizeof(float);
     float *h_send = nullptr, *h_recv = nullptr, *d_send = nullptr, *d_recv = nullptr;
     HIP_OK(hipHostMalloc((void**)&h_send, bytes, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void**)&h_recv, bytes, hipHostMallocDefault));

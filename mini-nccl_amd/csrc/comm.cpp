@@ -402,6 +402,16 @@ ncclResult_t Comm::check_status() {
     fprintf(stderr, "[Mini-NCCL] rank %d: all-reduce %s (status 0x%x); communicator is no longer usable\n", rank_,
             (st & kStatusTimeout) ? "timed out (watchdog)" : (st & kStatusHostAbort) ? "aborted by host" : "aborted by a peer",
             st);
+    if ((st & kStatusRemoteAbort) && !(st & (kStatusTimeout | kStatusHostAbort))) {
+      // the ABORT word the first aborting peer wrote (kernels.hip abort_word; the host's
+      // abort_peers writes rank + 1 only)
+      const uint64_t a = reinterpret_cast<const volatile uint64_t*>(h_ctl_ + 4)[3];
+      const uint32_t why = (uint32_t)(a >> 32);
+      if (a)
+        fprintf(stderr, "[Mini-NCCL] rank %d: first abort came from rank %d (%s)\n", rank_, (int)(a & 0xffffffffu) - 1,
+                (why & kStatusTimeout) ? "its watchdog timed out" : (why & kStatusHostAbort) ? "its host aborted"
+                : (why & kStatusRemoteAbort) ? "relaying an abort" : "it gave up outside its kernel");
+    }
     if (st & kStatusTimeout) {
       // which mailbox word the first timed-out wait was stuck on (kernels.hip record_timeout)
       const volatile uint64_t* diag = reinterpret_cast<const volatile uint64_t*>(h_ctl_ + 4);
@@ -672,7 +682,7 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
 }
 
 void Comm::abort_peers() {
-  static const uint64_t one = 1;
+  const uint64_t one = (uint64_t)(rank_ + 1);  // kernels.hip abort_word, with no kernel status
   hipStream_t st = nullptr;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
     (void)hipGetLastError();

@@ -196,8 +196,19 @@ __device__ __noinline__ bool wait_ge_spin(const u64* flag, u64 target, const Ctl
     __builtin_amdgcn_s_sleep(1);
     if (ld_sys(flag) >= target) return true;
     if ((polls & 63) == 0) {
-      if (ld_sys(c.my_abort) != 0) { st_sys32(c.status, kStatusRemoteAbort); return false; }
-      if (ld_sys32(c.host_abort) != 0) { st_sys32(c.status, kStatusHostAbort); return false; }
+      // the first cause stays in the status word (a peer's abort that echoes this rank's own
+      // timeout must not hide it); the peer's ABORT word names it and its cause (abort_word)
+      if (const u64 a = ld_sys(c.my_abort)) {
+        if (ld_sys32(c.status) == 0) {
+          __hip_atomic_store(reinterpret_cast<u64*>(c.status + 4) + 3, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          st_sys32(c.status, kStatusRemoteAbort);
+        }
+        return false;
+      }
+      if (ld_sys32(c.host_abort) != 0) {
+        if (ld_sys32(c.status) == 0) st_sys32(c.status, kStatusHostAbort);
+        return false;
+      }
       if (ld_sys32(c.status) != 0) return false;  // a sibling workgroup gave up
       if (__builtin_amdgcn_s_memrealtime() - t0 > c.timeout_ticks) {
         record_timeout(c, flag, target, ld_sys(flag));
@@ -328,9 +339,15 @@ __device__ __forceinline__ void move(const char* lsrc, char* ldst, rsrc_t in, rs
   else move_scalar<T, OPC, KIND>(lsrc, ldst, in, out, nbytes, lane, 0);
 }
 
+// the ABORT word a giving-up rank writes into its peers' mailboxes: its rank + 1 (never 0) and
+// its own status (why it gave up) -- the peers report both (Comm::check_status)
+__device__ __forceinline__ u64 abort_word(const CollParams& p) {
+  return ((u64)ld_sys32(p.status) << 32) | (u64)(p.rank + 1);
+}
+
 __device__ __forceinline__ void abort_peers(const CollParams& p, int C, int a, int b) {
-  st_sys(p.peer_mbox[a] + mbox_abort(p.n, C), 1ull);
-  st_sys(p.peer_mbox[b] + mbox_abort(p.n, C), 1ull);
+  st_sys(p.peer_mbox[a] + mbox_abort(p.n, C), abort_word(p));
+  st_sys(p.peer_mbox[b] + mbox_abort(p.n, C), abort_word(p));
 }
 
 // the host watchdog's deadline starts when the kernel does (Comm::wait_for): one posted write
@@ -353,8 +370,16 @@ __device__ __forceinline__ WaveId wave_id() {
 }
 
 // ---------------------------------------------------------------- ring kernel
+// Every rank's persistent kernel waits for its peers' kernels, so on a GPU that several rank
+// processes share (the reference's perf_test topology, the one-GPU test box) all of them must be
+// resident at once: 8 ranks x 256 one-wave pipelines = 2 waves on each of the 1024 SIMDs.  The
+// collective kernels therefore ask for >= 2 waves per SIMD (<= 256 VGPRs + AGPRs per wave; a
+// read-kernel variant at 256 + 1 AGPR fitted only one, and 8 co-located ranks crawled until
+// their watchdogs fired).  With one rank per GPU this costs nothing.
+constexpr int kMinWavesPerSimd = 2;
+
 template <typename T, int OPC, bool VEC>
-__global__ void __launch_bounds__(kMaxThreads) ring_kernel(CollParams p) {
+__global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) ring_kernel(CollParams p) {
   signal_start(p);
   const WaveId id = wave_id();
   const int lane = id.lane, w = id.w, C = id.C;
@@ -523,7 +548,7 @@ constexpr int kMaxWaves = kMaxThreads / 64;
 constexpr int kPushU = MNCCL_PUSH_U;
 
 template <typename T, int OPC, bool VEC>
-__global__ void __launch_bounds__(kMaxThreads) direct_kernel(CollParams p) {
+__global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) direct_kernel(CollParams p) {
   signal_start(p);
   const WaveId id = wave_id();
   const int lane = id.lane, w = id.w, C = id.C, wv = id.wv;
@@ -641,7 +666,7 @@ __global__ void __launch_bounds__(kMaxThreads) direct_kernel(CollParams p) {
   return;
 aborted:
   if (lane == 0)
-    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), 1ull);
+    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), abort_word(p));
 }
 
 // ---------------------------------------------------------------- read kernel
@@ -751,6 +776,61 @@ __device__ __forceinline__ void read_copy_wide(const CollParams& p, uint64_t sof
   }
 }
 
+// The fold of a slice from 4 to 8 ranks (a node): each batch loads V vectors per lane from EVERY
+// peer at once, and the next batch's loads leave before this batch is folded (two register
+// sets).  The fold's order is fixed (ring order), its load order is not: loaded one peer after
+// the other, every wave of every rank would start its batches at peer r+1 and the ranks'
+// incoming traffic would sit on one link at a time -- over xGMI, a seventh of a rank's links
+// at 8 ranks; loaded together, every link carries its share all the time.  G peer slots, V
+// vectors: (n-1) x V KiB per batch, two batches in flight per wave (4-5 ranks: 4 KiB per peer,
+// 6-8 ranks: 3 KiB; both within the kernel's 256 VGPRs without spilling).  At 2 and 3 ranks
+// (one or two links) the one-peer-ahead batches below keep more bytes in flight per stream.
+#ifndef MNCCL_READ_FOLD_ALL
+#define MNCCL_READ_FOLD_ALL 1
+#endif
+
+template <typename T, int OPC, int G, int V>
+__device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff, uint32_t nvec, int lane) {
+  constexpr uint32_t S = 64 * V;
+  const int n = p.n, r = p.rank;
+  const uint32_t vb = nvec * 16;
+  const rsrc_t loc = make_rsrc(p.send + coff, vb), out = make_rsrc(p.recv + coff, vb);
+  rsrc_t in[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) in[g] = make_rsrc(p.peer_send[direct_peer(n, r, 1 + (g + 1 < n ? g : 0))] + coff, vb);
+  v4u xa[G][V], aa[V], xb[G][V], ab[V];
+  auto load = [&](v4u(&x)[G][V], v4u(&a)[V], uint32_t b) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      if (g + 1 < n) {
+#pragma unroll
+        for (int u = 0; u < V; ++u) x[g][u] = ld_slot16(in[g], (b + (uint32_t)(u * 64 + lane)) * 16);
+      }
+#pragma unroll
+    for (int u = 0; u < V; ++u) a[u] = ld_nt16(loc, (b + (uint32_t)(u * 64 + lane)) * 16);
+  };
+  auto fold_store = [&](v4u(&x)[G][V], v4u(&a)[V], uint32_t b) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      if (g + 1 < n) {
+#pragma unroll
+        for (int u = 0; u < V; ++u) a[u] = reduce16<T, OPC>(x[g][u], a[u]);
+      }
+#pragma unroll
+    for (int u = 0; u < V; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, a[u]);
+  };
+  uint32_t b = 0;
+  load(xa, aa, 0);
+  for (;;) {
+    if (b + S < nvec) load(xb, ab, b + S);
+    fold_store(xa, aa, b);
+    if ((b += S) >= nvec) break;
+    if (b + S < nvec) load(xa, aa, b + S);
+    fold_store(xb, ab, b);
+    if ((b += S) >= nvec) break;
+  }
+}
+
 template <typename T, int OPC, bool VEC>
 __device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, uint32_t nbytes, int lane) {
   if (!VEC) {
@@ -758,10 +838,19 @@ __device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, ui
     return;
   }
   const int n = p.n, r = p.rank;
+  const uint32_t nvec = nbytes >> 4;
+  if (MNCCL_READ_FOLD_ALL && n >= 4 && n <= 8) {
+    // (2-byte types widen to f32 in reduce16: one vector fewer per peer keeps the bf16 / fp16
+    // variants within 256 registers without spilling)
+    constexpr int h = sizeof(T) == 2 ? 1 : 0;
+    if (nvec && n <= 5) read_fold_all<T, OPC, 4, 4 - h>(p, coff, nvec, lane);
+    else if (nvec) read_fold_all<T, OPC, 7, 3 - h>(p, coff, nvec, lane);
+    if (nbytes & 15u) read_fold_scalar<T, OPC>(p, coff, nbytes, lane, nvec * 16);
+    return;
+  }
   constexpr int U = kReadFoldU;
   const rsrc_t out = make_rsrc(p.recv + coff, nbytes);
   const char* lsrc = p.send + coff;
-  const uint32_t nvec = nbytes >> 4;
   uint32_t b = 0;
   // full batches: the n-1 remote streams are issued back to back (one peer ahead of the fold)
   for (; b + 64 * U <= nvec; b += 64 * U) {
@@ -798,7 +887,7 @@ __device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, ui
 // awaited.  DONE also returns credits for every message (the scratch schedules' slot counters
 // continue across calls, whatever the schedule).
 template <typename T, int OPC, bool VEC>
-__global__ void __launch_bounds__(kMaxThreads) read_kernel(CollParams p) {
+__global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(CollParams p) {
   signal_start(p);
   const WaveId id = wave_id();
   const int lane = id.lane, w = id.w, C = id.C, wv = id.wv;
@@ -881,7 +970,7 @@ __global__ void __launch_bounds__(kMaxThreads) read_kernel(CollParams p) {
   return;
 aborted:
   if (lane == 0)
-    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), 1ull);
+    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), abort_word(p));
 }
 
 // ---------------------------------------------------------------- local reduce

@@ -158,7 +158,20 @@ char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHa
     peers_.erase(peers_.begin() + (long)lru);
   }
   void* p = nullptr;
-  const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  // an open can fail transiently while the runtime finishes a close; retry a few times before
+  // failing the call (every failure and retry is reported)
+  for (int attempt = 1; e != hipSuccess && attempt <= 5; ++attempt) {
+    (void)hipGetLastError();
+    char hx[129];
+    for (int i = 0; i < 64; ++i) snprintf(hx + 2 * i, 3, "%02x", (unsigned char)h.reserved[i]);
+    fprintf(stderr,
+            "[Mini-NCCL] rank %d: hipIpcOpenMemHandle of rank %d's allocation (base 0x%llx, id %llu) failed: %s; "
+            "%zu mappings open, handle %s; retry %d\n",
+            rank_, q, (unsigned long long)base, (unsigned long long)id, hipGetErrorString(e), peers_.size(), hx, attempt);
+    usleep(1000u << attempt);
+    e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  }
   if (e != hipSuccess) {
     (void)hipGetLastError();
     throw std::runtime_error(std::string("read schedule: hipIpcOpenMemHandle of rank ") + std::to_string(q) +

@@ -1,0 +1,69 @@
+"""Resource budget of the shipped gfx950 kernels, read from the built library (CPU only).
+
+The persistent collective kernels (ring / direct / read) of every rank must be resident on the
+GPU at the same time: each waits for its peers' kernels.  With 8 rank processes sharing one GPU
+(the reference's perf_test topology) that is 8 x 256 one-wave pipelines = 2 waves on each of
+the 1024 SIMDs, so no collective kernel may use more than 256 registers per lane (VGPRs +
+AGPRs); and none may use scratch memory (a spill inside the message loop costs a memory round
+trip per access).  Checked from the code object's own metadata (.vgpr_count, .agpr_count,
+.private_segment_fixed_size) -- no compile and no GPU needed.
+"""
+import os
+import re
+import struct
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "mini-nccl_amd", "lib", "libmini_nccl.so")
+READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+
+
+def _gfx950_code_object(path):
+    """The gfx950 entry of the clang offload bundle embedded in the library's .hip_fatbin."""
+    data = open(path, "rb").read()
+    i = data.find(b"__CLANG_OFFLOAD_BUNDLE__")
+    assert i >= 0, "no offload bundle in the library"
+    n = struct.unpack_from("<Q", data, i + 24)[0]
+    off = i + 32
+    for _ in range(n):
+        eo, es, idl = struct.unpack_from("<QQQ", data, off)
+        tid = data[off + 24:off + 24 + idl].decode()
+        off += 24 + idl
+        if "gfx950" in tid and es:
+            return data[i + eo:i + eo + es]
+    raise AssertionError("no gfx950 code object in the bundle")
+
+
+def _kernels(tmp_path):
+    co = tmp_path / "co.elf"
+    co.write_bytes(_gfx950_code_object(LIB))
+    out = subprocess.run([READELF, "--notes", str(co)], capture_output=True, text=True, check=True).stdout
+    kernels, cur = {}, None
+    for line in out.splitlines():
+        m = re.match(r"\s*-?\s*\.(agpr_count|name|private_segment_fixed_size|vgpr_count):\s+(\S+)", line)
+        if not m:
+            continue
+        key, val = m.groups()
+        if line.lstrip().startswith("-"):  # a new kernel record starts
+            cur = {}
+        if cur is None:
+            continue
+        cur[key] = val
+        if "name" in cur and all(k in cur for k in ("agpr_count", "vgpr_count", "private_segment_fixed_size")):
+            kernels[cur["name"]] = {k: int(v) for k, v in cur.items() if k != "name"}
+            cur = None
+    return kernels
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(READELF)), reason="library not built / no llvm-readelf")
+def test_collective_kernels_fit_two_waves_per_simd_without_scratch(tmp_path):
+    ks = _kernels(tmp_path)
+    coll = {k: v for k, v in ks.items() if re.search(r"(ring|direct|read)_kernel", k)}
+    # 3 schedules x 5 dtypes x 4 ops x (vector, scalar) instantiations
+    assert len(coll) == 120, sorted(coll)[:5]
+    over = {k: v for k, v in coll.items() if v["vgpr_count"] + v["agpr_count"] > 256}
+    assert not over, f"collective kernels above 256 registers (1 wave per SIMD): {over}"
+    spill = {k: v for k, v in ks.items() if v["private_segment_fixed_size"] != 0}
+    assert not spill, f"kernels using scratch memory: {spill}"
