@@ -534,7 +534,10 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
                                          cfg_.pipe_depth > 1 ? cfg_.pipe_depth : kReadDepth)
                             : effective_slice(chunk_bytes, C, wave_slice(), cfg_.min_slice, cfg_.pipe_depth);
   p.nslices = (chunk_bytes + p.slice_bytes - 1) / p.slice_bytes;
-  p.iters = (uint32_t)((p.nslices + (uint64_t)C - 1) / (uint64_t)C);
+  // the read kernel runs one pipeline per slice up to C (schedule.h read_pipelines)
+  const int A = algo == 2 ? read_pipelines(p.nslices, C, geo_.waves) : C;
+  p.iters = (uint32_t)((p.nslices + (uint64_t)A - 1) / (uint64_t)A);
+  p.pipes = C;
   p.n = n;
   p.rank = rank_;
   p.nslots = cfg_.slots;
@@ -556,7 +559,7 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.sys_fence = cfg_.sys_fence;
   p.direct_overlap = cfg_.direct_overlap;
   p.pull = cfg_.pull;
-  const int nt = cfg_.threads, wg = geo_.workgroups;
+  const int nt = cfg_.threads, wg = algo == 2 ? A / geo_.waves : geo_.workgroups;
   hipError_t e = algo == 2   ? launch_read(dtype, op, vec, wg, nt, p, stream)
                  : algo == 1 ? launch_direct(dtype, op, vec, wg, nt, p, stream)
                              : launch_ring(dtype, op, vec, wg, nt, p, stream);

@@ -33,6 +33,8 @@ struct CollParams {
   int32_t sys_fence;       // system-scope release fence before each ready flag
   int32_t direct_overlap;  // direct: next iteration's raw pushes before this one's results
   int32_t pull;            // slots in the sender's scratch, loaded over the link (schedule.h)
+  int32_t pipes;           // the communicator's pipelines (mailbox / counter layout); the read
+                           // kernel's grid may run fewer (schedule.h read_pipelines)
   const char* peer_send[16];  // read schedule: every rank's send buffer, mapped here (own at [rank])
   const char* peer_recv[16];  // read schedule: every rank's recv buffer, mapped here
 };

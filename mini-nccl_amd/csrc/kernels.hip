@@ -890,7 +890,9 @@ template <typename T, int OPC, bool VEC>
 __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(CollParams p) {
   signal_start(p);
   const WaveId id = wave_id();
-  const int lane = id.lane, w = id.w, C = id.C, wv = id.wv;
+  // C: the communicator's pipelines (mailbox and counter layout); A: the ones this call runs
+  // (its grid), slice s on pipeline s mod A
+  const int lane = id.lane, w = id.w, C = p.pipes, A = id.C, wv = id.wv;
   const int n = p.n, r = p.rank;
   __shared__ u64 s_tx[kMaxWaves][kMaxRanks], s_rx[kMaxWaves][kMaxRanks];
   u64* tx = s_tx[wv];
@@ -913,7 +915,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
   for (uint32_t j = 0; j <= iters; ++j) {
     if (j < iters) {
       // F(j): fold my chunk's slice j from the peers' send buffers, store, drain, READY
-      const u64 s = (u64)j * C + w;
+      const u64 s = (u64)j * A + w;
       const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
       if (len) read_fold<T, OPC, VEC>(p, (u64)r * p.chunk_bytes + s * p.slice_bytes, len, lane);
       drain_stores();
@@ -926,7 +928,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
       // (full batches peer by peer; the rest of the slice -- all of a short one -- for every
       // peer at once, once all their READYs are in)
       const uint32_t t = j - 1;
-      const u64 s = (u64)t * C + w;
+      const u64 s = (u64)t * A + w;
       const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
       const uint32_t nvec = len >> 4;
       const uint32_t full = VEC ? nvec / (64u * kReadCopyU) * (64u * kReadCopyU) : 0;

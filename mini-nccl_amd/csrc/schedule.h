@@ -91,6 +91,18 @@ MNCCL_HD int direct_msgs_per_iter() { return 2; }  // per (pair, channel): raw, 
 // and call, all on the READY word: START, one per iteration (result slice ready), DONE.
 MNCCL_HD uint64_t read_msgs_per_call(uint32_t iters) { return (uint64_t)iters + 2; }
 
+// Pipelines a read-schedule call runs: one per slice, up to all C of them, rounded up to whole
+// workgroups of `waves` pipelines.  The others sit the call out on every rank alike (a pure
+// function of the call's size and the rank-uniform geometry), so their per-pair counters stay
+// in step; a small call then dispatches, handshakes and drains a few waves, not C.  Slice s of
+// a call goes to pipeline s mod A (iteration s / A).
+MNCCL_HD int read_pipelines(uint64_t nslices, int C, int waves) {
+  uint64_t a = nslices < (uint64_t)C ? nslices : (uint64_t)C;
+  if (a == 0) a = 1;
+  a = (a + (uint64_t)waves - 1) / (uint64_t)waves * (uint64_t)waves;
+  return a < (uint64_t)C ? (int)a : C;
+}
+
 // Direct phases of one pipeline, in execution order: A(t) pushes raw slices of iteration t,
 // B(t) folds and pushes results, C(t) copies the arriving results.  Plain order A0 B0 C0 A1 B1
 // C1 ...; overlapped order A0 B0 A1 C0 B1 A2 C1 ... B(I-1) C(I-1): the next iteration's raw

@@ -29,6 +29,7 @@ float apply(int op, float a, float b) {
 
 struct World {
   int n, C, K, op, algo, overlap = 1, pull = 0;
+  int A = 0;  // pipelines the current call runs (read: schedule.h read_pipelines; else C)
   uint64_t slice, slot_bytes, chunk_bytes, nslices;  // payload per message, slot stride
   uint32_t iters;
   std::vector<const float*> send;
@@ -198,7 +199,7 @@ bool read_step(World& W, Prog& P) {
     case 2: {
       if (P.k == 0) {
         if (P.it < W.iters) {
-          const uint64_t s = (uint64_t)P.it * W.C + w;
+          const uint64_t s = (uint64_t)P.it * W.A + w;
           const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
           const uint64_t coff = (uint64_t)r * W.chunk_bytes + s * W.slice;
           const float* local = (const float*)((const char*)W.send[r] + coff);
@@ -219,7 +220,7 @@ bool read_step(World& W, Prog& P) {
         const uint32_t t = P.it - 1;
         const int q = direct_peer(n, r, 1 + (P.k - 1 + w) % (n - 1));
         if (W.ready(r, q, w) < rx(q) + 2 + t) return false;
-        const uint64_t s = (uint64_t)t * W.C + w;
+        const uint64_t s = (uint64_t)t * W.A + w;
         const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
         const uint64_t coff = (uint64_t)q * W.chunk_bytes + s * W.slice;
         memcpy((char*)W.recv[r] + coff, (const char*)W.recv[q] + coff, len);
@@ -306,7 +307,8 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
     else if (a == 2) W.slice = read_slice(W.chunk_bytes, channels, slice_bytes, min_slice, kReadDepth);
     else W.slice = effective_slice(W.chunk_bytes, channels, slice_bytes, min_slice, 1);
     W.nslices = (W.chunk_bytes + W.slice - 1) / W.slice;
-    W.iters = (uint32_t)((W.nslices + (uint64_t)channels - 1) / (uint64_t)channels);
+    W.A = a == 2 ? read_pipelines(W.nslices, channels, 1) : channels;  // as Comm::launch
+    W.iters = (uint32_t)((W.nslices + (uint64_t)W.A - 1) / (uint64_t)W.A);
     for (int r = 0; r < n; ++r) {  // send -> recv copy of the tail (Comm::allreduce)
       if ((const void*)recv[r] == (const void*)send[r]) continue;  // in place
       const uint64_t body = W.chunk_bytes * (uint64_t)n;
@@ -319,7 +321,7 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
       for (int w = 0; w < channels; ++w) {
         Prog p;
         p.r = r; p.w = w;
-        p.done = W.iters == 0;
+        p.done = W.iters == 0 || w >= W.A;  // pipelines past A sit the call out
         progs.push_back(p);
       }
     for (;;) {
@@ -349,7 +351,7 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
     }
     // the kernels' last action per channel: advance the per-pair FIFO counters
     for (int r = 0; r < n; ++r)
-      for (int w = 0; w < channels; ++w) {
+      for (int w = 0; w < W.A; ++w) {
         if (a == 2) {
           for (int q = 0; q < n; ++q) {
             if (q == r) continue;

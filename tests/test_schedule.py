@@ -206,3 +206,18 @@ def test_read_slice_properties(sim_lib, chunk, C):
         assert -(-per_pipe // e) >= 16 or e == sl and -(-per_pipe // e) >= 1
     if e < 16384:
         assert e == S.effective_slice(chunk, C, sl, floor)
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+def test_read_small_calls_run_only_the_pipelines_they_need(oracle_lib, sim_lib, n):
+    # schedule.h read_pipelines: a read call with fewer slices than pipelines runs one pipeline per
+    # slice; the rest sit it out on every rank, so their per-pair counters stay in step through
+    # later calls of any schedule (ring and direct run every pipeline, idle ones included)
+    C, count = 8, n * 48  # 192 B chunks of 64 B slices: 3 slices, 3 of the 8 pipelines
+    xs = O.random_inputs(n, count, "f32", seed=40 + n)
+    ref = O.allreduce(xs, slice_bytes=64)
+    _, steps = S.allreduce(xs, algo=2, slice_bytes=64, channels=C)
+    assert steps == n * 3 * (4 + 1 + 1 + (n - 1))  # iters = 1 on 3 pipelines
+    for seed in range(3):
+        got, _ = S.allreduce(xs, slice_bytes=64, channels=C, algos=[2, 0, 2, 1, 2, 2, 0, 1, 2], seed=seed + 1)
+        assert all(same_bits(g, e) for g, e in zip(got, ref))
