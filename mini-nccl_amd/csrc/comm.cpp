@@ -651,6 +651,12 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
         // kernel's own wait would (the reference's 10 s watchdog, mini_nccl.cu:200-214)
         d = pbuf_.negotiate(send, recv, eligible, count, dtype, op, cfg_.timeout_ms / 1000.0 + 2.0,
                             [this] { wait_previous_call(); }, psend, precv, &vec_all, capturing);
+      } catch (const PeerGaveUp& e) {
+        // a peer's communicator died in an earlier rendezvous: as a peer's ABORT in the kernel
+        fprintf(stderr, "[Mini-NCCL] rank %d: %s; communicator is no longer usable\n", rank_, e.what());
+        sticky_ = ncclRemoteError;
+        if (cur_dev != device_) hipSetDevice(cur_dev);
+        return sticky_;
       } catch (const std::exception& e) {
         fprintf(stderr, "[Mini-NCCL] rank %d: %s; communicator is no longer usable\n", rank_, e.what());
         sticky_ = ncclInternalError;

@@ -46,6 +46,10 @@ struct alignas(64) CallRec {
   uint64_t count;
   int32_t dtype, op, eligible, aligned;
   BufDesc send, recv;
+  // second round (only when some rank may have to open a new mapping): the call whose mapping
+  // outcome map_ok reports, stored after it (release)
+  alignas(64) std::atomic<uint64_t> mapped;
+  int32_t map_ok;
 };
 
 struct alignas(64) Counter {
@@ -55,6 +59,7 @@ struct alignas(64) Counter {
 struct Board {
   uint32_t magic, nranks;
   Counter consumed[kMaxRanks];  // last call whose records rank q has read
+  Counter gave_up[kMaxRanks];   // != 0: rank q abandoned a rendezvous (its communicator is dead)
   CallRec rec[kMaxRanks][kBoardDepth];
 };
 
@@ -114,6 +119,12 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
 }
 
 bool PeerBuffers::describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMemHandle_t* h) {
+  if (test_fake_) {  // CPU self-test: the pointer's page is its "allocation", the value its id
+    *base = (uint64_t)(uintptr_t)p & ~(uint64_t)4095;
+    *id = (uint64_t)(uintptr_t)p;
+    memset(h, 0, sizeof *h);
+    return true;
+  }
   hipDeviceptr_t b = 0;
   size_t sz = 0;
   unsigned long long bid = 0;
@@ -146,21 +157,16 @@ char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHa
       m.pinned = m.pinned || pin;
       return m.local;
     }
-  size_t unpinned = 0;
-  for (const Mapping& m : peers_) unpinned += m.pinned ? 0 : 1;
-  if (unpinned >= kMaxMappings) {
-    // least recently used (unpinned) out; the last kernel may still read through it
-    size_t lru = peers_.size();
-    for (size_t i = 0; i < peers_.size(); ++i)
-      if (!peers_[i].pinned && (lru == peers_.size() || peers_[i].last_use < peers_[lru].last_use)) lru = i;
-    sync_previous();
-    (void)hipIpcCloseMemHandle(peers_[lru].local);
-    peers_.erase(peers_.begin() + (long)lru);
+  if (test_fake_) {  // CPU self-test: no HIP; fail on the chosen call
+    if (seq_ == test_fail_call_) throw std::runtime_error("read schedule: injected mapping failure (self-test)");
+    peers_.push_back(Mapping{q, base, id, (char*)(uintptr_t)base, seq_, pin});
+    if (peers_.size() > kMaxMappings) peers_.erase(peers_.begin());
+    return (char*)(uintptr_t)base;
   }
   void* p = nullptr;
   hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-  // an open can fail transiently while the runtime finishes a close; retry a few times before
-  // failing the call (every failure and retry is reported)
+  // an open can fail transiently; retry a few times before failing the call (every failure
+  // and retry is reported)
   for (int attempt = 1; e != hipSuccess && attempt <= 5; ++attempt) {
     (void)hipGetLastError();
     char hx[129];
@@ -178,11 +184,26 @@ char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHa
                              "'s buffer: " + hipGetErrorString(e));
   }
   peers_.push_back(Mapping{q, base, id, (char*)p, seq_, pin});
+  // over the bound: the least recently used (unpinned) mapping goes, AFTER the new one is open
+  // (a close immediately followed by an open could hand the new import the address range the
+  // runtime is still releasing); the last kernel may still read through it, so wait for it
+  size_t unpinned = 0;
+  for (const Mapping& m : peers_) unpinned += m.pinned ? 0 : 1;
+  if (unpinned > kMaxMappings) {
+    size_t lru = peers_.size();
+    for (size_t i = 0; i < peers_.size(); ++i)
+      if (!peers_[i].pinned && (lru == peers_.size() || peers_[i].last_use < peers_[lru].last_use)) lru = i;
+    sync_previous();
+    (void)hipIpcCloseMemHandle(peers_[lru].local);
+    (void)hipGetLastError();
+    peers_.erase(peers_.begin() + (long)lru);
+  }
   return (char*)p;
 }
 
 void PeerBuffers::close_all() {
-  for (Mapping& m : peers_) (void)hipIpcCloseMemHandle(m.local);
+  if (!test_fake_)
+    for (Mapping& m : peers_) (void)hipIpcCloseMemHandle(m.local);
   peers_.clear();
   (void)hipGetLastError();
 }
@@ -192,16 +213,36 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
                                              const std::function<void()>& sync_previous, const char** psend,
                                              const char** precv, bool* vec_all, bool pin) {
   const uint64_t k = ++seq_;
-  const int slot = (int)(k % kBoardDepth);
   const double t0 = now_s();
   auto wait = [&](const std::atomic<uint64_t>& v, uint64_t want, int q, const char* what) {
     for (int spins = 0; v.load(std::memory_order_acquire) < want; ++spins) {
+      if (board_->gave_up[q].v.load(std::memory_order_acquire) != 0)
+        throw PeerGaveUp("read schedule: rank " + std::to_string(q) + " abandoned the communicator before all-reduce #" +
+                         std::to_string(k));
       if (now_s() - t0 > timeout_s)
         throw std::runtime_error("read schedule: rank " + std::to_string(q) + " did not " + what + " all-reduce #" +
                                  std::to_string(k) + " within " + std::to_string((int)timeout_s) + " s");
       backoff(spins);
     }
   };
+  try {
+    return negotiate_body(k, send, recv, eligible, count, dtype, op, sync_previous, psend, precv, vec_all, pin, wait);
+  } catch (const PeerGaveUp&) {
+    throw;
+  } catch (...) {
+    // this rank gives up (a peer that never came, a mapping that failed): say so on the board,
+    // so every peer waiting in a rendezvous with it fails at once instead of at its own limit
+    board_->gave_up[rank_].v.store(k, std::memory_order_release);
+    throw;
+  }
+}
+
+template <typename Wait>
+PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible,
+                                                  uint64_t count, int dtype, int op,
+                                                  const std::function<void()>& sync_previous, const char** psend,
+                                                  const char** precv, bool* vec_all, bool pin, const Wait& wait) {
+  const int slot = (int)(k % kBoardDepth);
   // my record slot is free once every peer has read the record kBoardDepth calls back
   if (k > (uint64_t)kBoardDepth)
     for (int q = 0; q < nranks_; ++q)
@@ -236,7 +277,6 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
     if (q != rank_) wait(c.seq, k, q, "reach");
     recs[(size_t)q] = Seen{c.count, c.dtype, c.op, c.eligible, c.aligned, c.send, c.recv};
   }
-  board_->consumed[rank_].v.store(k, std::memory_order_release);  // my copies are taken
   bool all = true, mismatch = false, aligned = true;
   for (const Seen& c : recs) {
     all = all && c.eligible;
@@ -244,7 +284,28 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
     mismatch = mismatch || c.count != count || c.dtype != dtype || c.op != op;
   }
   const Decision d = mismatch ? kMismatch : all ? kRead : kFallback;
-  if (d != kRead) return d;
+  if (d != kRead) {
+    board_->consumed[rank_].v.store(k, std::memory_order_release);  // my copies are taken
+    return d;
+  }
+  // Would any rank have to open a mapping?  Every buffer used by a read call in the last
+  // `horizon` read calls is still mapped by every other rank (each keeps its kMaxMappings most
+  // recently used; those calls used at most 2(n-1) per rank), so if every buffer of this call is
+  // among them, no rank opens anything -- the common case of a caller reusing its buffers -- and
+  // no second round is needed.  Computed from the records alone: every rank reaches the same
+  // answer.
+  const size_t horizon = kMaxMappings / (size_t)(2 * (nranks_ > 1 ? nranks_ - 1 : 1));
+  auto recent = [&](int q, const BufDesc& b) {
+    for (const auto& call : recent_)
+      for (const RecentKey& x : call)
+        if (x.rank == q && x.base == b.base && x.id == b.id) return true;
+    return false;
+  };
+  bool need_agree = false;
+  for (int q = 0; q < nranks_ && !need_agree; ++q)
+    need_agree = !recent(q, recs[(size_t)q].send) || !recent(q, recs[(size_t)q].recv);
+  bool mapped = true;
+  std::string why;
   for (int q = 0; q < nranks_; ++q) {
     const Seen& c = recs[(size_t)q];
     if (q == rank_ || nonces_[(size_t)q] == nonces_[(size_t)rank_]) {
@@ -252,11 +313,47 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
       precv[q] = (const char*)(uintptr_t)c.recv.raw;
       continue;
     }
-    psend[q] = map_peer(q, c.send.base, c.send.id, c.send.h, sync_previous, pin) + c.send.off;
-    precv[q] = map_peer(q, c.recv.base, c.recv.id, c.recv.h, sync_previous, pin) + c.recv.off;
+    if (!mapped) continue;
+    try {
+      psend[q] = map_peer(q, c.send.base, c.send.id, c.send.h, sync_previous, pin) + c.send.off;
+      precv[q] = map_peer(q, c.recv.base, c.recv.id, c.recv.h, sync_previous, pin) + c.recv.off;
+    } catch (const std::runtime_error& e) {
+      if (!need_agree) throw;  // cannot happen (nothing new to open); fail loudly if it does
+      mapped = false;
+      why = e.what();
+    }
+  }
+  Decision out = kRead;
+  if (need_agree) {
+    // second round: every rank's mapping outcome; one failure -> the scratch schedule for this
+    // call on every rank (same bits, no buffer of a peer is read)
+    ++agreements_;
+    me.map_ok = mapped ? 1 : 0;
+    me.mapped.store(k, std::memory_order_release);
+    int failed = -1;
+    for (int q = 0; q < nranks_; ++q) {
+      const CallRec& c = board_->rec[q][slot];
+      if (q != rank_) wait(c.mapped, k, q, "report its mappings for");
+      if (!c.map_ok && failed < 0) failed = q;
+    }
+    if (failed >= 0) {
+      fprintf(stderr, "[Mini-NCCL] rank %d: all-reduce #%llu falls back to the scratch schedule: rank %d could not map "
+              "a peer's buffer%s%s\n", rank_, (unsigned long long)k, failed, why.empty() ? "" : ": ", why.c_str());
+      out = kFallback;
+    }
+  }
+  board_->consumed[rank_].v.store(k, std::memory_order_release);  // my copies are taken
+  if (out == kRead) {
+    std::vector<RecentKey> keys;
+    for (int q = 0; q < nranks_; ++q) {
+      keys.push_back(RecentKey{q, recs[(size_t)q].send.base, recs[(size_t)q].send.id});
+      keys.push_back(RecentKey{q, recs[(size_t)q].recv.base, recs[(size_t)q].recv.id});
+    }
+    recent_.push_back(std::move(keys));
+    while (recent_.size() > horizon) recent_.pop_front();
   }
   *vec_all = aligned;
-  return d;
+  return out;
 }
 
 }  // namespace mnccl

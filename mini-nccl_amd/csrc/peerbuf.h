@@ -19,7 +19,9 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include <deque>
 #include <functional>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -28,6 +30,11 @@
 namespace mnccl {
 
 struct Board;  // shared-memory layout (peerbuf.cpp)
+
+// A peer abandoned the communicator in an earlier rendezvous (its calls fail from now on).
+struct PeerGaveUp : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
 
 class PeerBuffers {
  public:
@@ -57,6 +64,14 @@ class PeerBuffers {
 
   // for tests / diagnostics
   size_t mapped_allocations() const { return peers_.size(); }
+  uint64_t agreements() const { return agreements_; }  // calls that needed the mapping round
+  // CPU self-test only (no GPU): describe() returns synthetic (base, id) from the pointer value,
+  // map_peer() returns the owner's raw address, and map_peer() fails on call `fail_call` (0:
+  // never), as a failed hipIpcOpenMemHandle would
+  void set_test_fake(bool fake, uint64_t fail_call) {
+    test_fake_ = fake;
+    test_fail_call_ = fail_call;
+  }
 
  private:
   struct Export {
@@ -70,6 +85,10 @@ class PeerBuffers {
     uint64_t last_use;
     bool pinned;        // used by a captured graph: never evicted
   };
+  template <typename Wait>
+  Decision negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible, uint64_t count, int dtype,
+                          int op, const std::function<void()>& sync_previous, const char** psend, const char** precv,
+                          bool* vec_all, bool pin, const Wait& wait);
   bool describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMemHandle_t* h);
   char* map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h,
                  const std::function<void()>& sync_previous, bool pin);
@@ -81,6 +100,14 @@ class PeerBuffers {
   uint64_t seq_ = 0;  // calls negotiated so far
   std::vector<Export> exports_;
   std::vector<Mapping> peers_;
+  struct RecentKey {
+    int rank;
+    uint64_t base, id;
+  };
+  std::deque<std::vector<RecentKey>> recent_;  // buffers of the last read calls (every rank alike)
+  uint64_t agreements_ = 0;
+  bool test_fake_ = false;
+  uint64_t test_fail_call_ = 0;
 };
 
 }  // namespace mnccl

@@ -433,6 +433,12 @@ int mnccl_board_selftest(int rank, int nranks, const char* ip, int port, int sce
     mnccl::PeerBuffers pb;
     pb.init(b, rank, nranks, nonces, port);
     if (!pb.available()) return -3;
+    // scenarios 4 / 5: every rank eligible with synthetic buffers (no HIP); 4: rank 1 cannot map
+    // on call 3 (every rank must fall back on that call alone); 5: the same buffers every call
+    // after the first (the mapping round runs once), except a fresh buffer on call calls/2
+    std::vector<char> arena(1 << 20);
+    const bool fake = scenario == 4 || scenario == 5;
+    if (fake) pb.set_test_fake(true, scenario == 4 && rank == 1 ? 3u : 0u);
     uint64_t rng = 0x9E3779B97F4A7C15ull * (uint64_t)(rank + 1);
     for (int i = 0; i < calls; ++i) decisions[i] = 99;
     for (int i = 0; i < calls; ++i) {
@@ -446,7 +452,18 @@ int mnccl_board_selftest(int rank, int nranks, const char* ip, int port, int sce
       const char* pr[mnccl::kMaxRanks] = {};
       bool vec = false;
       try {
-        decisions[i] = (int)pb.negotiate(nullptr, nullptr, false, count, 7, 0, timeout_s, [] {}, ps, pr, &vec);
+        const void* sb = nullptr;
+        void* rb = nullptr;
+        if (scenario == 4) {  // a new send / recv page every call
+          sb = arena.data() + (size_t)(2 * i) * 4096 % arena.size();
+          rb = arena.data() + (size_t)(2 * i + 1) * 4096 % arena.size();
+        } else if (scenario == 5) {
+          const int gen = i == calls / 2 ? 1 : 0;
+          sb = arena.data() + (size_t)(2 * gen) * 4096;
+          rb = arena.data() + (size_t)(2 * gen + 1) * 4096;
+        }
+        decisions[i] = (int)pb.negotiate(sb, rb, fake, count, 7, 0, timeout_s, [] {}, ps, pr, &vec);
+        if (fake) decisions[i] += 10 * (int)pb.agreements();  // decision + 10 x mapping rounds so far
       } catch (const std::runtime_error&) {
         decisions[i] = -9;
         break;

@@ -100,3 +100,28 @@ def test_read_schedule_rendezvous_across_processes(sim_lib, world, scenario):
             if scenario == 1:
                 exp[calls // 2] = -1
             assert dec == exp, (r, dec)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("scenario", [4, 5], ids=["map-failure", "reused-buffers"])
+def test_read_schedule_mapping_round(sim_lib, world, scenario):
+    # csrc/peerbuf.cpp's second round, one process per rank, no GPU (synthetic buffers): when a
+    # call brings a buffer no read call used recently, every rank reports whether it could map
+    # its peers' buffers before any launches; one failure (rank 1, call 3: an injected
+    # hipIpcOpenMemHandle failure) -> the scratch schedule (0) for that call on EVERY rank and
+    # the read schedule (1) on every other call; buffers reused call after call -> the round
+    # runs only for the calls that bring a new buffer.  dec[i] = decision + 10 x rounds so far.
+    import gpu_workers as GW
+    calls = 24
+    port = GW.free_port()
+    out = GW.run_ranks(_board_rank, world, lambda r: (r, world, port, scenario, calls), 120)
+    assert sorted(out) == list(range(world)), out
+    for r in range(world):
+        assert "error" not in out[r], out[r].get("error")
+        assert out[r]["rc"] == 0, out[r]
+        dec = out[r]["dec"]
+        if scenario == 4:
+            exp = [(0 if i == 2 else 1) + 10 * (i + 1) for i in range(calls)]
+        else:
+            exp = [1 + 10 * (1 if i < calls // 2 else 2) for i in range(calls)]
+        assert dec == exp, (r, dec)
