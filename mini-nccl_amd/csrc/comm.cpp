@@ -142,7 +142,6 @@ void Comm::setup_device_resources() {
   hip_check(hipHostMalloc((void**)&h_ctl_, 4096, hipHostMallocMapped | hipHostMallocCoherent), "alloc ctl");
   memset(h_ctl_, 0, 4096);
   hip_check(hipHostGetDevicePointer((void**)&d_ctl_, h_ctl_, 0), "ctl device pointer");
-  hip_check(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "event");
   hip_check(hipEventCreateWithFlags(&order_ev_, hipEventDisableTiming), "event");
   if (nranks_ > 1) {
     hip_check(hipExtMallocWithFlags((void**)&scratch_, scratch_bytes_, hipDeviceMallocUncached), "alloc scratch");
@@ -343,7 +342,6 @@ Comm::~Comm() {
   // the last call may still run (stream-ordered mode): its kernel writes into the peers' scratch
   // and mailboxes, which they free after the barrier below -- wait for it first
   if (have_last_ && order_ev_) hipEventSynchronize(order_ev_);
-  if (done_) hipEventSynchronize(done_);
   if (nranks_ > 1 && !peer_scratch_.empty()) {
     try {
       if (sticky_ == ncclSuccess) boot_.barrier();  // nobody still writes into my memory
@@ -382,7 +380,6 @@ void Comm::release() {
   if (stage_) hipFree(stage_);
   stage_ = nullptr;
   stage_bytes_ = 0;
-  if (done_) hipEventDestroy(done_);
   if (order_ev_) hipEventDestroy(order_ev_);
   order_ev_ = nullptr;
   have_last_ = false;
@@ -390,7 +387,6 @@ void Comm::release() {
   mbox_ = nullptr;
   pair_seq_ = nullptr;
   h_ctl_ = nullptr;
-  done_ = nullptr;
   (void)hipGetLastError();
 }
 
@@ -439,12 +435,14 @@ ncclResult_t Comm::async_error() {
 // raise the abort word the kernel polls.  Work ahead of the kernel on the stream is the caller's
 // and is waited for without a deadline (the abort word could not reach it anyway).
 ncclResult_t Comm::wait_for(hipStream_t stream, uint32_t seq) {
-  hip_check(hipEventRecord(done_, stream), "event record");
+  // order_ev_ was recorded on `stream` right after this call's work (allreduce): it is the
+  // completion event too (one event record per call, ~1.8 us each on MI355X)
+  (void)stream;
   double t0 = -1.0;
   const double limit = cfg_.timeout_ms / 1000.0 + 2.0;
   bool aborted = false;
   for (int spins = 0;; ++spins) {
-    hipError_t q = hipEventQuery(done_);
+    hipError_t q = hipEventQuery(order_ev_);
     if (q == hipSuccess) break;
     if (q != hipErrorNotReady) hip_check(q, "stream query");
     if (t0 < 0.0) {

@@ -100,8 +100,8 @@ class Comm {
   char* stage_ = nullptr;         // device staging copy for pageable host buffers (grown on demand)
   size_t stage_bytes_ = 0;
 
-  hipEvent_t done_ = nullptr;
-  hipEvent_t order_ev_ = nullptr;     // recorded after every call (cross-stream ordering)
+  hipEvent_t order_ev_ = nullptr;     // recorded after every call: cross-stream ordering, and the
+                                      // blocking call's completion (wait_for)
   hipStream_t last_stream_ = nullptr;
   bool have_last_ = false;
   ncclResult_t sticky_ = ncclSuccess;
