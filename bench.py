@@ -680,7 +680,10 @@ def main():
     else:
         comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
         info = comm.info()
-        if args.algo == "auto":
+        # auto: the library's own choice, measured choice (MINI_NCCL_CALIBRATE) included; the
+        # schedule it ran is read back after the run
+        auto_mode = args.algo == "auto"
+        if auto_mode:
             args.algo = ALGO_NAMES[info["algo"]]
         send = torch.ones(count, device=dev, dtype=tdt)
         recv = torch.empty(count, device=dev, dtype=tdt)
@@ -693,8 +696,8 @@ def main():
                     raise M.NcclError(rc, "ncclAllReduce")
             return step
 
-        def run_algo(algo):
-            comm.set_algo(ALGO_NAMES.index(algo))
+        def run_algo(algo, auto=False):
+            comm.set_algo(M.ALGO_AUTO if auto else ALGO_NAMES.index(algo))
             step = make_step()
             recv.fill_(-1.0)
             for _ in range(max(1, args.warmup)):
@@ -707,7 +710,11 @@ def main():
             # then 3 calls on varying data (outside the timed region), restoring the buffers
             ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream,
                                     barrier=dist.barrier)
-            ok = ok and comm.info()["last_algo"] == ALGO_NAMES.index(algo)  # no fallback happened
+            i = comm.info()
+            if auto:  # the measured choice when decided, else the default read
+                ok = ok and i["last_algo"] == (i["calib_choice"] if i["calib_choice"] >= 0 else ALGO_NAMES.index("read"))
+            else:
+                ok = ok and i["last_algo"] == ALGO_NAMES.index(algo)  # no fallback happened
             send.fill_(1.0)
             ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
             return max_over_ranks(wall), max_over_ranks(ev_ms), ok
@@ -741,7 +748,17 @@ def main():
                 link["topology_rank0"] = peer_topology(local_rank, n, args.same_device)
             except Exception as e:
                 link["topology_rank0"] = {"error": str(e)[:120]}
-        wall, ev_ms, ok = run_algo(args.algo)
+        wall, ev_ms, ok = run_algo(args.algo, auto=auto_mode)
+        calib = None
+        if auto_mode:
+            i = comm.info()
+            args.algo = ALGO_NAMES[i["last_algo"]]  # what the timed calls ran
+            calib = ({"choice": ALGO_NAMES[i["calib_choice"]], "read_ms": round(i["calib_ms"][0], 4),
+                      ALGO_NAMES[i["scratch_algo"]] + "_ms": round(i["calib_ms"][1], 4),
+                      "rule": "MINI_NCCL_CALIBRATE: large auto calls 0-2 run read (warm-up), the scratch schedule "
+                              "and read (timed); every rank's timings travel with its call records; later large "
+                              "calls run the scratch schedule only if it is >= 3 % faster (max over ranks)"}
+                     if i["calib_choice"] >= 0 else "off or undecided")
         ms = wall / args.steps * 1e3
         algbw = nbytes / (ms / 1e3) / 1e9
         alg_bytes = 3 * esz * (n - 1) * (count // n)
@@ -757,7 +774,8 @@ def main():
                        "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
                        "algo_rule": "MINI_NCCL_ALGO=auto: read (peers' buffers loaded over the links, no scratch) "
                                     "for device buffers; otherwise direct from 3 ranks on more than one GPU, else "
-                                    "ring (no all-reduce at init)"},
+                                    "ring (no all-reduce at init)",
+                       "calibration": calib},
             "busbw": round(algbw * 2 * (n - 1) / n, 3),
         })
         # ceiling of each schedule from the probed links (min over ranks): ring moves
@@ -791,7 +809,7 @@ def main():
                     result["alt"].append({"algo": other, "error": str(e)[:200]})
                 if rank == 0:
                     arm(result)
-            comm.set_algo(ALGO_NAMES.index(args.algo))
+            comm.set_algo(M.ALGO_AUTO if auto_mode else ALGO_NAMES.index(args.algo))
         # rank 0's kernel, measured where this run runs (ranks sharing one GPU: the proxy entry)
         traffic, tsrc = pmc_traffic(f"{args.algo}_{args.dtype}_1GiB_n{n}" + ("_same_gpu" if args.same_device else ""))
         kern_key = f"{args.algo}_kernel"

@@ -26,6 +26,10 @@ extern "C" {
 
 /* schedules; all produce bit-identical results (same fold order per element) */
 typedef enum {
+  mncclAlgoAuto = -1,  /* the library's default: read for device buffers; with
+                          MINI_NCCL_CALIBRATE (on by default when the ranks span more than one
+                          GPU) the first calls of at least MINI_NCCL_CALIBRATE_BYTES time read
+                          against the scratch schedule and later such calls run the faster */
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
   mncclAlgoDirect = 1, /* every peer pushes its slice of chunk c straight to rank c over its
                           own xGMI link; c folds them in ring order c, c+1, ..., c-1 and
@@ -65,6 +69,10 @@ typedef struct {
   size_t peer_mappings;   /* read schedule: peer allocations mapped into this process */
   int scratch_algo;       /* the read schedule's fallback (ring or direct), chosen from the
                              ranks' GPUs: direct from 3 ranks on more than one GPU */
+  int calib_choice;       /* MINI_NCCL_CALIBRATE: schedule kept for large calls (mncclAlgo_t), -1
+                             while undecided or when calibration is off */
+  double calib_ms[2];     /* the timings it was decided on: read, scratch schedule (ms per call,
+                             max over ranks); 0 until decided */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,
@@ -74,7 +82,8 @@ ncclResult_t mncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError);
 
 ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info);
 
-/* every rank must make the same choice before its next all-reduce */
+/* every rank must make the same choice before its next all-reduce; mncclAlgoAuto restores the
+   default (and its calibration) */
 ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo);
 
 /* Collective diagnostic: every rank streams `bytes` (0 = its whole scratch region) into the

@@ -163,6 +163,9 @@ ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info) {
   info->last_algo = c->last_algo();
   info->peer_mappings = c->peer_mappings();
   info->scratch_algo = c->scratch_algo();
+  info->calib_choice = c->calib_choice();
+  info->calib_ms[0] = c->calib_ms(0);
+  info->calib_ms[1] = c->calib_ms(1);
   return ncclSuccess;
 }
 
@@ -170,7 +173,8 @@ ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info) {
 // schedules' messages share mailboxes and slots), as with any other communicator setting.
 ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo) {
   if (!comm) return ncclInvalidArgument;
-  if (algo != mncclAlgoRing && algo != mncclAlgoDirect && algo != mncclAlgoRead) return ncclInvalidArgument;
+  if (algo != mncclAlgoRing && algo != mncclAlgoDirect && algo != mncclAlgoRead && algo != mncclAlgoAuto)
+    return ncclInvalidArgument;
   reinterpret_cast<Comm*>(comm)->set_algo(algo);
   return ncclSuccess;
 }

@@ -99,7 +99,8 @@ struct PeerInfo {
   int32_t channels, slots, threads, abi;
   int32_t window, signal_batch, algo, tune;
   uint64_t min_slice, tune_bytes;
-  int32_t depth, overlap, pull, pad1;
+  int32_t depth, overlap, pull, calibrate;
+  uint64_t calibrate_bytes;
   hipIpcMemHandle_t scratch_h, mbox_h;
   uint64_t scratch_ptr, mbox_ptr;  // raw addresses for ranks living in the same process
 };
@@ -113,6 +114,7 @@ Comm::Comm(int nranks, int rank, const std::string& ip) : rank_(rank), nranks_(n
   // when some rank's buffers cannot be shared) -- the scratch schedule is decided from the
   // peers' devices in exchange_and_map
   algo_ = cfg_.algo >= 0 ? cfg_.algo : 2;
+  algo_auto_ = cfg_.algo < 0;
   scratch_algo_ = cfg_.algo == 1 ? 1 : 0;
   if (nranks > kMaxRanks) throw std::invalid_argument("nRanks > 16 is not supported on one node");
   geo_ = pipeline_geometry(nranks, cfg_.channels, cfg_.threads, cfg_.window_size, cfg_.signal_batch, cfg_.slots,
@@ -193,6 +195,8 @@ void Comm::exchange_and_map() {
   me.depth = cfg_.pipe_depth;
   me.overlap = cfg_.direct_overlap;
   me.pull = cfg_.pull;
+  me.calibrate = cfg_.calibrate;
+  me.calibrate_bytes = cfg_.calibrate_bytes;
   hip_check(hipIpcGetMemHandle(&me.scratch_h, scratch_), "ipc handle scratch");
   hip_check(hipIpcGetMemHandle(&me.mbox_h, mbox_), "ipc handle mailbox");
   me.scratch_ptr = (uint64_t)(uintptr_t)scratch_;
@@ -209,10 +213,12 @@ void Comm::exchange_and_map() {
     if (p.slice != me.slice || p.channels != me.channels || p.slots != me.slots || p.threads != me.threads ||
         p.window != me.window || p.signal_batch != me.signal_batch || p.scratch_cap != me.scratch_cap ||
         p.min_slice != me.min_slice || p.depth != me.depth || p.overlap != me.overlap || p.pull != me.pull ||
-        p.algo != me.algo || p.tune != me.tune || p.tune_bytes != me.tune_bytes || p.abi != me.abi)
+        p.algo != me.algo || p.tune != me.tune || p.tune_bytes != me.tune_bytes || p.abi != me.abi ||
+        p.calibrate != me.calibrate || p.calibrate_bytes != me.calibrate_bytes)
       throw std::invalid_argument(
           "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SIGNAL_BATCH / SLOTS / CHANNELS / THREADS / SCRATCH_MB / MIN_SLICE / "
-          "PIPE_DEPTH / DIRECT_OVERLAP / PULL / ALGO / TUNE / TUNE_BYTES differ between ranks");
+          "PIPE_DEPTH / DIRECT_OVERLAP / PULL / ALGO / TUNE / TUNE_BYTES / CALIBRATE / CALIBRATE_BYTES differ between "
+          "ranks");
   }
   // the scratch schedule of MINI_NCCL_ALGO=auto / read (the read schedule's fallback), the same
   // on every rank (computed from the gathered records): from 3 ranks, `direct` when the ranks are
@@ -228,6 +234,10 @@ void Comm::exchange_and_map() {
   }
   const int rule = (nranks_ >= 3 && !one_device) ? 1 : 0;
   if (cfg_.algo < 0 || cfg_.algo == 2) scratch_algo_ = rule;
+  // measured choice between read and the scratch schedule for large calls: by default where the
+  // links decide it (ranks on more than one GPU); on one GPU read always wins (it moves half the
+  // HBM bytes), so it is off there unless MINI_NCCL_CALIBRATE=1
+  calib_on_ = cfg_.calibrate == 1 || (cfg_.calibrate < 0 && !one_device);
   // Rank PROCESSES sharing this GPU: a persistent kernel waits for its peers' kernels, so all of
   // them must be resident at once; the GPU's scheduler maps a bounded number of processes and
   // hardware queues together, beyond which it time-slices and every hand-off waits for a turn
@@ -381,6 +391,11 @@ void Comm::release() {
   stage_ = nullptr;
   stage_bytes_ = 0;
   if (order_ev_) hipEventDestroy(order_ev_);
+  for (auto& pair : calib_ev_)
+    for (hipEvent_t& e : pair) {
+      if (e) hipEventDestroy(e);
+      e = nullptr;
+    }
   order_ev_ = nullptr;
   have_last_ = false;
   scratch_ = nullptr;
@@ -638,17 +653,23 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     int algo = algo_ == 2 ? scratch_algo_ : algo_;
     const char* psend[kMaxRanks] = {};
     const char* precv[kMaxRanks] = {};
+    int measure = -1;  // calibration: this call's kernel is timed as read (0) / scratch schedule (1)
     if (algo_ == 2 && pbuf_.available()) {
       // the read schedule: every rank takes part in the rendezvous, all decide alike
       // a captured call reads through mappings its replays keep using: they are pinned
       const bool eligible = ksend == send && krecv == recv && device_local(send) && device_local(recv);
       bool vec_all = false;
       PeerBuffers::Decision d = PeerBuffers::kFallback;
+      // large auto calls while the measured choice is open (the same predicate on every rank)
+      const bool large = calib_on_ && algo_auto_ && !capturing && bytes >= cfg_.calibrate_bytes;
+      const bool calib = large && calib_choice_ < 0;
+      float max_t[2] = {0.f, 0.f};
+      if (calib) poll_calibration();
       try {
         // a peer that does not reach the call within the watchdog's limit fails it, as the
         // kernel's own wait would (the reference's 10 s watchdog, mini_nccl.cu:200-214)
         d = pbuf_.negotiate(send, recv, eligible, count, dtype, op, cfg_.timeout_ms / 1000.0 + 2.0,
-                            [this] { wait_previous_call(); }, psend, precv, &vec_all, capturing);
+                            [this] { wait_previous_call(); }, psend, precv, &vec_all, capturing, my_t_, max_t);
       } catch (const PeerGaveUp& e) {
         // a peer's communicator died in an earlier rendezvous: as a peer's ABORT in the kernel
         fprintf(stderr, "[Mini-NCCL] rank %d: %s; communicator is no longer usable\n", rank_, e.what());
@@ -670,12 +691,37 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
       }
       if (d == PeerBuffers::kRead) {
         algo = 2;
-        vec = vec_all && (chunk_bytes % 4 == 0);
+        if (calib) {
+          if (max_t[0] > 0.f && max_t[1] > 0.f) {
+            // every rank's timings are in: keep the scratch schedule only if it is clearly faster
+            calib_ms_[0] = max_t[0];
+            calib_ms_[1] = max_t[1];
+            calib_choice_ = max_t[1] < 0.97f * max_t[0] ? scratch_algo_ : 2;
+            if (cfg_.debug && rank_ == 0)
+              fprintf(stderr, "[Mini-NCCL] calibration: read %.3f ms, %s %.3f ms per call -> %s\n", max_t[0],
+                      scratch_algo_ ? "direct" : "ring", max_t[1], calib_choice_ == 2 ? "read" : "scratch schedule");
+          } else {
+            measure = calib_large_ == 1 ? 1 : calib_large_ == 2 ? 0 : -1;
+            if (calib_large_ == 1) algo = scratch_algo_;
+            ++calib_large_;
+          }
+        }
+        if (large && calib_choice_ >= 0) algo = calib_choice_;
+        if (algo == 2) vec = vec_all && (chunk_bytes % 4 == 0);
       }
     }
     seq = ++call_seq_;
     if (seq == 0) seq = ++call_seq_;  // 0 = "no kernel" (wait_for)
+    if (measure >= 0) {
+      for (hipEvent_t& e : calib_ev_[measure])
+        if (!e) hip_check(hipEventCreate(&e), "calibration event");
+      hip_check(hipEventRecord(calib_ev_[measure][0], stream), "calibration event");
+    }
     launch(algo, ksend, krecv, chunk_bytes, dtype, op, stream, seq, vec, psend, precv);
+    if (measure >= 0) {
+      hip_check(hipEventRecord(calib_ev_[measure][1], stream), "calibration event");
+      calib_rec_[measure] = true;
+    }
     if (rr == Reach::kStaged) hip_check(hipMemcpyAsync(recv, stage_, bytes, hipMemcpyDefault, stream), "stage out");
   }
   if (!capturing) {
@@ -686,6 +732,18 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
   if (cur_dev != device_) hipSetDevice(cur_dev);
   if (cfg_.blocking && cap == hipStreamCaptureStatusNone) return wait_for(stream, seq);
   return ncclSuccess;
+}
+
+void Comm::poll_calibration() {
+  for (int m = 0; m < 2; ++m) {
+    if (!calib_rec_[m] || my_t_[m] > 0.f) continue;
+    const hipError_t q = hipEventQuery(calib_ev_[m][1]);
+    if (q == hipErrorNotReady) continue;
+    float ms = 0.f;
+    if (q == hipSuccess && hipEventElapsedTime(&ms, calib_ev_[m][0], calib_ev_[m][1]) == hipSuccess)
+      my_t_[m] = ms > 1e-3f ? ms : 1e-3f;
+    (void)hipGetLastError();
+  }
 }
 
 void Comm::abort_peers() {

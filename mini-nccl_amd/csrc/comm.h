@@ -33,7 +33,13 @@ class Comm {
   int device() const { return device_; }
   const Config& config() const { return cfg_; }
   int algo() const { return algo_; }
-  void set_algo(int a) { algo_ = a; }
+  // a < 0: the default (read, measured choice for large calls when calibration is on)
+  void set_algo(int a) {
+    algo_auto_ = a < 0;
+    algo_ = a < 0 ? 2 : a;
+  }
+  int calib_choice() const { return calib_choice_; }
+  double calib_ms(int i) const { return calib_ms_[i & 1]; }
   int last_algo() const { return last_algo_; }  // schedule of the last launched kernel, -1: none
   size_t peer_mappings() const { return pbuf_.mapped_allocations(); }
   int scratch_algo() const { return scratch_algo_; }
@@ -68,6 +74,8 @@ class Comm {
   bool device_local(const void* p) const;  // device memory of this rank's GPU (not managed)
   void wait_previous_call();
   ncclResult_t check_status();
+  // MINI_NCCL_CALIBRATE: read the timings of this rank's measured calls whose events completed
+  void poll_calibration();
   // a rank that gives up on a call outside its kernel (the read schedule's rendezvous) raises
   // every peer's ABORT word, as a timed-out kernel does, so the peers fail fast instead of
   // running into their own watchdog
@@ -79,6 +87,17 @@ class Comm {
   int algo_ = 0;                 // 0 ring, 1 direct, 2 read
   int last_algo_ = -1;
   int scratch_algo_ = 0;         // ring or direct: the read schedule's fallback (and auto's rule)
+  // measured choice (MINI_NCCL_CALIBRATE): large auto calls 0, 1, 2 run read (warm-up), the
+  // scratch schedule (timed), read (timed); every rank publishes its timings with its call
+  // records and all decide alike once every rank's are in
+  bool algo_auto_ = false;       // MINI_NCCL_ALGO=auto and no explicit mncclCommSetAlgo
+  bool calib_on_ = false;
+  int calib_large_ = 0;          // large auto calls so far (the same count on every rank)
+  int calib_choice_ = -1;        // schedule kept for large calls; -1 undecided
+  double calib_ms_[2] = {0.0, 0.0};
+  float my_t_[2] = {0.f, 0.f};   // this rank's timings: read, scratch schedule (ms; 0 unknown)
+  hipEvent_t calib_ev_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  bool calib_rec_[2] = {false, false};
   int ranks_on_device_ = 1;
   uint32_t call_seq_ = 0;        // kernel launches of this communicator (the kernel's start word)
   double tune_ms_[2] = {0.0, 0.0};

@@ -77,6 +77,10 @@ Config Config::from_env() {
   if (tb < (1LL << 20)) tb = 1LL << 20;
   c.tune_bytes = (size_t)(tb & ~255LL);
   c.stage_host = env_int("MINI_NCCL_STAGE_HOST", 0) != 0;
+  if (const char* cal = std::getenv("MINI_NCCL_CALIBRATE"); cal && *cal && strcmp(cal, "auto") != 0)
+    c.calibrate = env_int("MINI_NCCL_CALIBRATE", -1) != 0 ? 1 : 0;
+  long long cb = env_int("MINI_NCCL_CALIBRATE_BYTES", 64LL << 20);
+  c.calibrate_bytes = (size_t)(cb < 1 ? 1 : cb);
   c.timeout_ms = (double)env_int("MINI_NCCL_TIMEOUT_MS", 10000);
   if (c.timeout_ms < 1) c.timeout_ms = 1;
   c.port = (int)env_int("MINI_NCCL_PORT", 8888);
@@ -89,10 +93,11 @@ std::string Config::describe() const {
   char b[384];
   snprintf(b, sizeof b,
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, scratch_cap=%zu MiB, algo=%s, "
-           "blocking=%d, sys_fence=%d, min_slice=%zu, depth=%d, pull=%d, tune=%d, stage_host=%d, timeout=%.0f ms, port=%d",
+           "blocking=%d, sys_fence=%d, min_slice=%zu, depth=%d, pull=%d, tune=%d, stage_host=%d, calibrate=%d (%zu B), "
+           "timeout=%.0f ms, port=%d",
            slice_size, window_size, signal_batch, slots, channels, threads, scratch_cap >> 20,
            algo < 0 ? "auto" : algo == 2 ? "read" : algo ? "direct" : "ring", blocking,
-           sys_fence, min_slice, pipe_depth, pull, tune, stage_host, timeout_ms, port);
+           sys_fence, min_slice, pipe_depth, pull, tune, stage_host, calibrate, calibrate_bytes, timeout_ms, port);
   return b;
 }
 

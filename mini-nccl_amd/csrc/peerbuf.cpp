@@ -46,6 +46,7 @@ struct alignas(64) CallRec {
   uint64_t count;
   int32_t dtype, op, eligible, aligned;
   BufDesc send, recv;
+  float t[2];  // this rank's calibration timings so far (Comm: read, scratch schedule; 0 = unknown)
   // second round (only when some rank may have to open a new mapping): the call whose mapping
   // outcome map_ok reports, stored after it (release)
   alignas(64) std::atomic<uint64_t> mapped;
@@ -211,7 +212,8 @@ void PeerBuffers::close_all() {
 PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv, bool eligible, uint64_t count,
                                              int dtype, int op, double timeout_s,
                                              const std::function<void()>& sync_previous, const char** psend,
-                                             const char** precv, bool* vec_all, bool pin) {
+                                             const char** precv, bool* vec_all, bool pin, const float* my_t,
+                                             float* max_t) {
   const uint64_t k = ++seq_;
   const double t0 = now_s();
   auto wait = [&](const std::atomic<uint64_t>& v, uint64_t want, int q, const char* what) {
@@ -226,7 +228,8 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
     }
   };
   try {
-    return negotiate_body(k, send, recv, eligible, count, dtype, op, sync_previous, psend, precv, vec_all, pin, wait);
+    return negotiate_body(k, send, recv, eligible, count, dtype, op, sync_previous, psend, precv, vec_all, pin,
+                          my_t, max_t, wait);
   } catch (const PeerGaveUp&) {
     throw;
   } catch (...) {
@@ -241,7 +244,8 @@ template <typename Wait>
 PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible,
                                                   uint64_t count, int dtype, int op,
                                                   const std::function<void()>& sync_previous, const char** psend,
-                                                  const char** precv, bool* vec_all, bool pin, const Wait& wait) {
+                                                  const char** precv, bool* vec_all, bool pin, const float* my_t,
+                                                  float* max_t, const Wait& wait) {
   const int slot = (int)(k % kBoardDepth);
   // my record slot is free once every peer has read the record kBoardDepth calls back
   if (k > (uint64_t)kBoardDepth)
@@ -264,6 +268,8 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
   me.aligned = ((sd.raw | rd.raw) % 4 == 0) ? 1 : 0;
   me.send = sd;
   me.recv = rd;
+  me.t[0] = my_t ? my_t[0] : 0.f;
+  me.t[1] = my_t ? my_t[1] : 0.f;
   me.seq.store(k, std::memory_order_release);
 
   struct Seen {
@@ -272,11 +278,19 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
     BufDesc send, recv;
   };
   std::vector<Seen> recs((size_t)nranks_);
+  float tmax[2] = {0.f, 0.f};
+  bool tall[2] = {true, true};
   for (int q = 0; q < nranks_; ++q) {
     const CallRec& c = board_->rec[q][slot];
     if (q != rank_) wait(c.seq, k, q, "reach");
     recs[(size_t)q] = Seen{c.count, c.dtype, c.op, c.eligible, c.aligned, c.send, c.recv};
+    for (int i = 0; i < 2; ++i) {
+      tall[i] = tall[i] && c.t[i] > 0.f;
+      tmax[i] = c.t[i] > tmax[i] ? c.t[i] : tmax[i];
+    }
   }
+  if (max_t)  // every rank's timing known -> their max (what every rank reads alike), else 0
+    for (int i = 0; i < 2; ++i) max_t[i] = tall[i] ? tmax[i] : 0.f;
   bool all = true, mismatch = false, aligned = true;
   for (const Seen& c : recs) {
     all = all && c.eligible;

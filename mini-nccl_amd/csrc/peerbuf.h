@@ -56,9 +56,12 @@ class PeerBuffers {
   // closed).  Throws std::runtime_error when a peer does not arrive within timeout_s.
   // `pin`: the call is being captured into a graph whose replays will read through these
   // mappings: they are never evicted (closed only with the communicator).
+  // my_t / max_t (optional): two timings this rank publishes with its record, and per timing
+  // the max over every rank's published value, or 0 while some rank's is still unknown (0).
   Decision negotiate(const void* send, const void* recv, bool eligible, uint64_t count, int dtype, int op,
                      double timeout_s, const std::function<void()>& sync_previous, const char** psend,
-                     const char** precv, bool* vec_all, bool pin = false);
+                     const char** precv, bool* vec_all, bool pin = false, const float* my_t = nullptr,
+                     float* max_t = nullptr);
   // Unmaps every peer allocation; call when no kernel of this communicator can still run.
   void close_all();
 
@@ -88,7 +91,7 @@ class PeerBuffers {
   template <typename Wait>
   Decision negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible, uint64_t count, int dtype,
                           int op, const std::function<void()>& sync_previous, const char** psend, const char** precv,
-                          bool* vec_all, bool pin, const Wait& wait);
+                          bool* vec_all, bool pin, const float* my_t, float* max_t, const Wait& wait);
   bool describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMemHandle_t* h);
   char* map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h,
                  const std::function<void()>& sync_previous, bool pin);

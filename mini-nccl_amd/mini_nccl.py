@@ -36,7 +36,7 @@ ncclFloat16, ncclFloat, ncclDouble, ncclBfloat16 = 6, 7, 8, 9
 ncclSum, ncclProd, ncclMax, ncclMin, ncclAvg = 0, 1, 2, 3, 4
 
 # mncclAlgo_t
-ALGO_RING, ALGO_DIRECT, ALGO_READ = 0, 1, 2
+ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_READ = -1, 0, 1, 2
 
 DTYPE_SIZE = {ncclInt32: 4, ncclFloat16: 2, ncclFloat: 4, ncclDouble: 8, ncclBfloat16: 2}
 
@@ -50,6 +50,7 @@ class CommInfo(ctypes.Structure):
         ("timeout_s", ctypes.c_double), ("scratch_bytes", ctypes.c_size_t), ("tune_ms", ctypes.c_double * 2),
         ("pipelines", ctypes.c_int), ("ranks_on_device", ctypes.c_int), ("slot_bytes", ctypes.c_size_t),
         ("last_algo", ctypes.c_int), ("peer_mappings", ctypes.c_size_t), ("scratch_algo", ctypes.c_int),
+        ("calib_choice", ctypes.c_int), ("calib_ms", ctypes.c_double * 2),
     ]
 
 
@@ -133,6 +134,7 @@ class Comm:
         check(load().mncclCommGetInfo(self.handle, ctypes.byref(i)))
         d = {f: getattr(i, f) for f, _ in CommInfo._fields_}
         d["tune_ms"] = list(d["tune_ms"])
+        d["calib_ms"] = list(d["calib_ms"])
         return d
 
     PROBE_FORMS = {"sys": 0, "nt": 1, "plain": 2}
