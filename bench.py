@@ -735,10 +735,13 @@ def main():
             # other access forms over the same links (min over ranks), for the choice of form
             # only: push non-temporal / default policy, pull (loads over the link)
             var = {}
-            for name, form, pull in (("push_nt", "nt", False), ("push_plain", "plain", False),
-                                     ("pull_sys", "sys", True), ("pull_plain", "plain", True)):
+            # *_user: the peers' ordinary device memory (hipMalloc, what the read schedule loads
+            # from) instead of their uncached scratch
+            for name, form, pull, user in (("push_nt", "nt", False, False), ("push_plain", "plain", False, False),
+                                           ("pull_sys", "sys", True, False), ("pull_plain", "plain", True, False),
+                                           ("pull_sys_user", "sys", True, True), ("push_sys_user", "sys", False, True)):
                 for where, allp in (("next", False), ("mesh", True)):
-                    g = comm.link_probe(allp, 0, 10, form=form, pull=pull)
+                    g = comm.link_probe(allp, 0, 10, form=form, pull=pull, user=user)
                     var[f"{where}_{name}"] = round(max_over_ranks(-g) * -1, 2)
             link["probe_variants_GBps_per_link"] = var
         except Exception as e:
@@ -786,7 +789,8 @@ def main():
             direct_ceiling = link["probe_mesh_GBps_per_link"] * n / 2
             link.update({"ring_ceiling_GBps": round(ring_ceiling, 2), "direct_ceiling_GBps": round(direct_ceiling, 2)})
             ceiling = direct_ceiling if args.algo == "direct" else ring_ceiling
-            pull = link.get("probe_variants_GBps_per_link", {}).get("mesh_pull_sys")
+            pv = link.get("probe_variants_GBps_per_link", {})
+            pull = pv.get("mesh_pull_sys_user") or pv.get("mesh_pull_sys")  # read loads user buffers
             if pull:
                 link["read_ceiling_GBps"] = round(pull * n / 2, 2)
                 if args.algo == "read":

@@ -92,8 +92,10 @@ ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo);
  * path's store form; *gbps = bytes per second per destination link.  Further bits of allPeers
  * select variants for comparison: bits 1-2 = the remote accesses' cache policy (0 = the hot
  * path's sc0 sc1, 1 = non-temporal, 2 = default), bit 3 = pull (load from the peers' scratch
- * over the link instead of storing into it).  Call only when no all-reduce is in flight on any
- * rank (it overwrites scratch slots). */
+ * over the link instead of storing into it), bit 4 = the peers' ordinary device memory (a
+ * hipMalloc buffer each rank exports for the probe -- what the read schedule loads from)
+ * instead of their uncached scratch.  Call only when no all-reduce is in flight on any rank (it
+ * overwrites scratch slots). */
 ncclResult_t mncclCommLinkProbe(ncclComm_t comm, int allPeers, size_t bytes, int iters, double* gbps);
 
 /* library version, 10000*major + 100*minor + patch */

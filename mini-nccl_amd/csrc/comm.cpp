@@ -763,10 +763,12 @@ void Comm::abort_peers() {
 
 ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gbps) {
   if (nranks_ < 2 || iters < 1) return ncclInvalidArgument;
-  // mode bits (mini_nccl_ext.h): 0 every peer, 1-2 access form, 3 pull instead of push
+  // mode bits (mini_nccl_ext.h): 0 every peer, 1-2 access form, 3 pull instead of push, 4 the
+  // peers' ordinary device memory instead of their scratch
   const int form = (all_peers >> 1) & 3;
   const bool pull = (all_peers >> 3) & 1;
-  if (form > kProbePlain || (all_peers & ~15)) return ncclInvalidArgument;
+  const bool user = (all_peers >> 4) & 1;
+  if (form > kProbePlain || (all_peers & ~31)) return ncclInvalidArgument;
   all_peers &= 1;
   const size_t region = scratch_region_bytes(wave_channels(), cfg_.slots, wave_slice());
   if (bytes == 0 || bytes > region) bytes = region;  // the probe writes this rank's region at each peer
@@ -780,10 +782,29 @@ ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gb
   hip_check(hipMalloc((void**)&src, bytes), "probe alloc");
   hip_check(hipMemsetAsync(src, 0x5a, bytes, st), "probe memset");
   std::vector<char*> dst;
+  // user memory: every rank exports a hipMalloc buffer of nranks x bytes; rank d's slice
+  // [rank * bytes, +bytes) is this rank's target there (as the scratch region is)
+  char* ub = nullptr;
+  std::vector<char*> opened((size_t)nranks_, nullptr);
+  if (user) {
+    hip_check(hipMalloc((void**)&ub, bytes * (size_t)nranks_), "probe user buffer");
+    hip_check(hipMemsetAsync(ub, 0x3c, bytes * (size_t)nranks_, st), "probe memset");
+    hipIpcMemHandle_t mine;
+    hip_check(hipIpcGetMemHandle(&mine, ub), "probe ipc handle");
+    std::vector<hipIpcMemHandle_t> all((size_t)nranks_);
+    boot_.allgather(&mine, all.data(), sizeof mine);
+    for (int q = 0; q < nranks_; ++q) {
+      if (q == rank_) continue;
+      void* p = nullptr;
+      hip_check(hipIpcOpenMemHandle(&p, all[(size_t)q], hipIpcMemLazyEnablePeerAccess), "probe ipc open");
+      opened[(size_t)q] = (char*)p;
+    }
+  }
   for (int k = 1; k < nranks_; ++k) {
     const int d = (rank_ + k) % nranks_;
     // in push mode this rank's region at d is where d receives from this rank
-    dst.push_back(peer_scratch_[(size_t)d] + (size_t)region_index(d, rank_) * region);
+    dst.push_back(user ? opened[(size_t)d] + (size_t)rank_ * bytes
+                       : peer_scratch_[(size_t)d] + (size_t)region_index(d, rank_) * region);
     if (!all_peers) break;
   }
   hipEvent_t e0, e1;
@@ -801,6 +822,12 @@ ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gb
   hip_check(hipEventElapsedTime(&ms, e0, e1), "event time");
   boot_.barrier();  // nobody starts an all-reduce while a peer still writes its slots
   *gbps = (double)bytes * iters / (ms * 1e-3) / 1e9;
+  if (user) {
+    for (char* p : opened)
+      if (p) (void)hipIpcCloseMemHandle(p);
+    boot_.barrier();  // every peer has unmapped my buffer before it is freed
+    hipFree(ub);
+  }
   hipEventDestroy(e0);
   hipEventDestroy(e1);
   hipStreamDestroy(st);

@@ -139,12 +139,13 @@ class Comm:
 
     PROBE_FORMS = {"sys": 0, "nt": 1, "plain": 2}
 
-    def link_probe(self, all_peers=False, nbytes=0, iters=10, form="sys", pull=False):
+    def link_probe(self, all_peers=False, nbytes=0, iters=10, form="sys", pull=False, user=False):
         """GB/s per destination link (collective: every rank must call it).  form: the remote
         accesses' cache policy ("sys" = the hot path's sc0 sc1, "nt", "plain"); pull: load
-        from the peers over the link instead of storing into them."""
+        from the peers over the link instead of storing into them; user: the peers' ordinary
+        device memory (what the read schedule loads from) instead of their uncached scratch."""
         g = ctypes.c_double()
-        mode = int(bool(all_peers)) | (self.PROBE_FORMS[form] << 1) | (8 if pull else 0)
+        mode = int(bool(all_peers)) | (self.PROBE_FORMS[form] << 1) | (8 if pull else 0) | (16 if user else 0)
         check(load().mncclCommLinkProbe(self.handle, mode, nbytes, iters, ctypes.byref(g)), "mncclCommLinkProbe")
         return g.value
 

@@ -303,8 +303,9 @@ def probe_rank(rank, n, port, env, out_q):
         comm = M.Comm(n, rank, "127.0.0.1")
         res = {"next": comm.link_probe(False, 8 << 20, 3), "mesh": comm.link_probe(True, 8 << 20, 3)}
         # the comparison forms (push nt / default policy, pull) on the same links
-        res["variants"] = [comm.link_probe(allp, 4 << 20, 2, form=f, pull=pl)
-                           for f, pl in (("nt", False), ("plain", False), ("sys", True), ("plain", True))
+        res["variants"] = [comm.link_probe(allp, 4 << 20, 2, form=f, pull=pl, user=u)
+                           for f, pl, u in (("nt", False, False), ("plain", False, False), ("sys", True, False),
+                                            ("plain", True, False), ("sys", True, True), ("sys", False, True))
                            for allp in (False, True)]
         count = 100003
         xs = O.random_inputs(n, count, "f32", seed=3)

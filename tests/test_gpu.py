@@ -397,7 +397,7 @@ def test_link_probe_then_allreduce(dev):
     for r in range(3):
         assert "error" not in out[r], out[r]["error"]
         assert out[r]["next"] > 0 and out[r]["mesh"] > 0
-        assert len(out[r]["variants"]) == 8 and all(g > 0 for g in out[r]["variants"])
+        assert len(out[r]["variants"]) == 12 and all(g > 0 for g in out[r]["variants"])
         assert out[r]["rc"] == 0 and out[r]["exact"]
 
 
