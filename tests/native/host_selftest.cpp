@@ -93,6 +93,24 @@ int main() {
       }
     }
   }
+  // the board's mapping round: 3 ranks as threads, synthetic buffers, rank 1 fails to map on
+  // call 3 -> that call falls back on every rank, every other call reads (decision + 10 x rounds)
+  {
+    std::vector<std::vector<int>> dec(3, std::vector<int>(24, -7));
+    std::vector<int> brc(3, -9);
+    std::vector<std::thread> bt;
+    for (int r = 0; r < 3; ++r)
+      bt.emplace_back([&, r] { brc[(size_t)r] = mnccl_board_selftest(r, 3, "127.0.0.1", port + 2, 4, 24, 10.0, dec[(size_t)r].data()); });
+    for (auto& t : bt) t.join();
+    for (int r = 0; r < 3; ++r) {
+      bool ok = brc[(size_t)r] == 0;
+      for (int i = 0; i < 24; ++i) ok = ok && dec[(size_t)r][(size_t)i] == (i == 2 ? 0 : 1) + 10 * (i + 1);
+      if (!ok) {
+        printf("mapping round FAIL rank %d rc=%d\n", r, brc[(size_t)r]);
+        ++fails;
+      }
+    }
+  }
   char buf[512];
   if (mnccl_config_describe(buf, (int)sizeof buf) != 0) {
     printf("config FAIL: %s\n", buf);
