@@ -698,6 +698,8 @@ def main():
 
         def run_algo(algo, auto=False):
             comm.set_algo(M.ALGO_AUTO if auto else ALGO_NAMES.index(algo))
+            if auto and os.environ.get("MNCCL_BENCH_FAIL_AUTO") == "1":  # rehearses the recovery below
+                raise M.NcclError(M.ncclInternalError, "injected (MNCCL_BENCH_FAIL_AUTO)")
             step = make_step()
             recv.fill_(-1.0)
             for _ in range(max(1, args.warmup)):
@@ -751,8 +753,28 @@ def main():
                 link["topology_rank0"] = peer_topology(local_rank, n, args.same_device)
             except Exception as e:
                 link["topology_rank0"] = {"error": str(e)[:120]}
-        wall, ev_ms, ok = run_algo(args.algo, auto=auto_mode)
         calib = None
+        try:
+            wall, ev_ms, ok = run_algo(args.algo, auto=auto_mode)
+        except M.NcclError as e:
+            # the measured choice times the scratch schedule during the warm-up; should that (or
+            # anything else in the auto run) kill the communicator -- every rank's calls fail
+            # alike, by the first timed step at the latest -- the line is still measured: a new
+            # communicator with the read schedule explicitly (the failure is on record)
+            if not auto_mode:
+                raise
+            log(f"headline with the library's choice failed ({e}); new communicator, read schedule")
+            calib = {"error": str(e)[:200], "fallback": "read schedule on a new communicator"}
+            try:
+                comm.destroy()
+            except Exception:
+                pass
+            os.environ["MINI_NCCL_CALIBRATE"] = "0"
+            torch.cuda.synchronize()
+            dist.barrier()
+            comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
+            auto_mode, args.algo = False, "read"
+            wall, ev_ms, ok = run_algo(args.algo)
         if auto_mode:
             i = comm.info()
             args.algo = ALGO_NAMES[i["last_algo"]]  # what the timed calls ran
