@@ -698,7 +698,8 @@ def main():
 
         def run_algo(algo, auto=False):
             comm.set_algo(M.ALGO_AUTO if auto else ALGO_NAMES.index(algo))
-            if auto and os.environ.get("MNCCL_BENCH_FAIL_AUTO") == "1":  # rehearses the recovery below
+            inj = os.environ.get("MNCCL_BENCH_FAIL_AUTO", "")  # rehearses the recovery below:
+            if (auto and inj in ("1", "2")) or (inj == "2" and algo == "read"):  # 2: read fails too
                 raise M.NcclError(M.ncclInternalError, "injected (MNCCL_BENCH_FAIL_AUTO)")
             step = make_step()
             recv.fill_(-1.0)
@@ -763,18 +764,29 @@ def main():
             # communicator with the read schedule explicitly (the failure is on record)
             if not auto_mode:
                 raise
-            log(f"headline with the library's choice failed ({e}); new communicator, read schedule")
-            calib = {"error": str(e)[:200], "fallback": "read schedule on a new communicator"}
-            try:
-                comm.destroy()
-            except Exception:
-                pass
+            calib = {"error": str(e)[:200]}
             os.environ["MINI_NCCL_CALIBRATE"] = "0"
-            torch.cuda.synchronize()
-            dist.barrier()
-            comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
-            auto_mode, args.algo = False, "read"
-            wall, ev_ms, ok = run_algo(args.algo)
+            auto_mode, last = False, e
+            # read first; should the read schedule itself be what fails, the scratch schedule
+            for alg in ("read", ALGO_NAMES[info["scratch_algo"]]):
+                log(f"headline failed ({last}); new communicator, {alg} schedule")
+                try:
+                    comm.destroy()
+                except Exception:
+                    pass
+                torch.cuda.synchronize()
+                dist.barrier()
+                comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
+                args.algo = alg
+                try:
+                    wall, ev_ms, ok = run_algo(alg)
+                    calib["fallback"] = f"{alg} schedule on a new communicator"
+                    break
+                except M.NcclError as e2:
+                    calib[f"{alg}_error"] = str(e2)[:200]
+                    last = e2
+            else:
+                raise last
         if auto_mode:
             i = comm.info()
             args.algo = ALGO_NAMES[i["last_algo"]]  # what the timed calls ran
