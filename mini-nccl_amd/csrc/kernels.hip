@@ -782,11 +782,15 @@ __device__ __forceinline__ void read_copy_wide(const CollParams& p, uint64_t sof
 // the other, every wave of every rank would start its batches at peer r+1 and the ranks'
 // incoming traffic would sit on one link at a time -- over xGMI, a seventh of a rank's links
 // at 8 ranks; loaded together, every link carries its share all the time.  G peer slots, V
-// vectors: (n-1) x V KiB per batch, two batches in flight per wave (4-5 ranks: 4 KiB per peer,
-// 6-8 ranks: 3 KiB; both within the kernel's 256 VGPRs without spilling).  At 2 and 3 ranks
-// (one or two links) the one-peer-ahead batches below keep more bytes in flight per stream.
+// vectors: (n-1) x V KiB per batch, two batches in flight per wave (2 ranks: 12 KiB, 3: 8 KiB
+// per peer, 4-5: 4 KiB, 6-8: 3 KiB; all within 256 registers without spilling).  Measured on
+// the one-GPU proxy against the one-peer-ahead batches below (used past 8 ranks): equal at 2
+// and 3 ranks (profiles/r2_read_fold_all_n23_ab.txt), 0.94-1.05x at 4 and 8.
 #ifndef MNCCL_READ_FOLD_ALL
 #define MNCCL_READ_FOLD_ALL 1
+#endif
+#ifndef MNCCL_FOLD_ALL_MIN_N
+#define MNCCL_FOLD_ALL_MIN_N 2
 #endif
 
 template <typename T, int OPC, int G, int V>
@@ -839,12 +843,15 @@ __device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, ui
   }
   const int n = p.n, r = p.rank;
   const uint32_t nvec = nbytes >> 4;
-  if (MNCCL_READ_FOLD_ALL && n >= 4 && n <= 8) {
-    // (2-byte types widen to f32 in reduce16: one vector fewer per peer keeps the bf16 / fp16
+  if (MNCCL_READ_FOLD_ALL && n >= MNCCL_FOLD_ALL_MIN_N && n <= 8) {
+    // (2-byte types widen to f32 in reduce16: fewer vectors per peer keep the bf16 / fp16
     // variants within 256 registers without spilling)
     constexpr int h = sizeof(T) == 2 ? 1 : 0;
-    if (nvec && n <= 5) read_fold_all<T, OPC, 4, 4 - h>(p, coff, nvec, lane);
-    else if (nvec) read_fold_all<T, OPC, 7, 3 - h>(p, coff, nvec, lane);
+    if (!nvec) {
+    } else if (n == 2) read_fold_all<T, OPC, 1, 12 - 4 * h>(p, coff, nvec, lane);
+    else if (n == 3) read_fold_all<T, OPC, 2, 8 - 2 * h>(p, coff, nvec, lane);
+    else if (n <= 5) read_fold_all<T, OPC, 4, 4 - h>(p, coff, nvec, lane);
+    else read_fold_all<T, OPC, 7, 3 - h>(p, coff, nvec, lane);
     if (nbytes & 15u) read_fold_scalar<T, OPC>(p, coff, nbytes, lane, nvec * 16);
     return;
   }
