@@ -201,6 +201,18 @@ def test_allreduce_8_ranks(dev, algo):
     _run_allreduce(8, cases, timeout=600)
 
 
+@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
+def test_allreduce_10_ranks(dev, algo):
+    # past a node's 8 ranks (up to 16 per communicator): the read kernel's one-peer-ahead fold and
+    # its peer groups of 7 in the short-slice forms; 10 rank processes on the one GPU with 64
+    # pipelines each and one hardware queue each (all resident at once), bit-exact vs the oracle
+    cases = [_case(count=10 * 70001 + 3, algo=algo, seed=12),                        # 1-2 KiB slices
+             _case(count=10 * (1 << 20), algo=algo, inplace=True, seed=13),          # full batches
+             _case(dtype="bf16", count=10 * 50007, algo=algo, seed=14)]
+    env = {"MINI_NCCL_CHANNELS": "64", "GPU_MAX_HW_QUEUES": "1"}
+    _run_allreduce(10, cases, env, timeout=600)
+
+
 def test_allreduce_8_ranks_c3_ring_128mib(dev):
     # C3's schedule (the reference's ring) in fp32 at 8 ranks on 128 MiB per rank: 16 MiB chunks,
     # every one of the 256 pipelines busy (64 KiB payloads), bit-exact vs the oracle
