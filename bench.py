@@ -792,9 +792,10 @@ def main():
             args.algo = ALGO_NAMES[i["last_algo"]]  # what the timed calls ran
             calib = ({"choice": ALGO_NAMES[i["calib_choice"]], "read_ms": round(i["calib_ms"][0], 4),
                       ALGO_NAMES[i["scratch_algo"]] + "_ms": round(i["calib_ms"][1], 4),
-                      "rule": "MINI_NCCL_CALIBRATE: large auto calls 0-2 run read (warm-up), the scratch schedule "
-                              "and read (timed); every rank's timings travel with its call records; later large "
-                              "calls run the scratch schedule only if it is >= 3 % faster (max over ranks)"}
+                      "rule": "MINI_NCCL_CALIBRATE: large auto calls 0-1 warm read and the scratch schedule up, "
+                              "2-3 time the scratch schedule and read; every rank's timings travel with its call "
+                              "records; later large calls run the scratch schedule only if it is >= 3 % faster "
+                              "(max over ranks)"}
                      if i["calib_choice"] >= 0 else "off or undecided")
         ms = wall / args.steps * 1e3
         algbw = nbytes / (ms / 1e3) / 1e9

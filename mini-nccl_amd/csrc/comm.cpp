@@ -701,8 +701,11 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
               fprintf(stderr, "[Mini-NCCL] calibration: read %.3f ms, %s %.3f ms per call -> %s\n", max_t[0],
                       scratch_algo_ ? "direct" : "ring", max_t[1], calib_choice_ == 2 ? "read" : "scratch schedule");
           } else {
-            measure = calib_large_ == 1 ? 1 : calib_large_ == 2 ? 0 : -1;
-            if (calib_large_ == 1) algo = scratch_algo_;
+            // large call 0: read (warms the peer mappings), 1: the scratch schedule (warms its
+            // remote scratch), 2: the scratch schedule timed, 3: read timed, then read until every
+            // rank's timings are in
+            measure = calib_large_ == 2 ? 1 : calib_large_ == 3 ? 0 : -1;
+            if (calib_large_ == 1 || calib_large_ == 2) algo = scratch_algo_;
             ++calib_large_;
           }
         }

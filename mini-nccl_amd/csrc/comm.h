@@ -87,9 +87,9 @@ class Comm {
   int algo_ = 0;                 // 0 ring, 1 direct, 2 read
   int last_algo_ = -1;
   int scratch_algo_ = 0;         // ring or direct: the read schedule's fallback (and auto's rule)
-  // measured choice (MINI_NCCL_CALIBRATE): large auto calls 0, 1, 2 run read (warm-up), the
-  // scratch schedule (timed), read (timed); every rank publishes its timings with its call
-  // records and all decide alike once every rank's are in
+  // measured choice (MINI_NCCL_CALIBRATE): large auto calls 0-3 run read and the scratch
+  // schedule once each to warm up, then each once timed; every rank publishes its timings with
+  // its call records and all decide alike once every rank's are in
   bool algo_auto_ = false;       // MINI_NCCL_ALGO=auto and no explicit mncclCommSetAlgo
   bool calib_on_ = false;
   int calib_large_ = 0;          // large auto calls so far (the same count on every rank)

@@ -162,19 +162,19 @@ def test_auto_tune_opt_in_picks_the_faster_schedule(dev):
 
 def test_measured_choice_between_read_and_scratch(dev):
     # MINI_NCCL_CALIBRATE (on by default when the ranks span several GPUs; forced here on the one
-    # GPU): large auto calls 0, 1, 2 run read (warm-up), the scratch schedule (timed) and read
-    # (timed); every rank publishes its timings with its call records, all decide alike on the
-    # first call where every rank's are in, and later large calls run the faster -- every call
-    # bit-exact vs the oracle
+    # GPU): large auto calls 0-3 run read and the scratch schedule to warm up, then the scratch
+    # schedule and read timed; every rank publishes its timings with its call records, all decide
+    # alike on the first call where every rank's are in, and later large calls run the faster --
+    # every call bit-exact vs the oracle
     n = 3
-    cases = [_case(count=1 << 20, algo=-1, seed=300 + i) for i in range(6)]
+    cases = [_case(count=1 << 20, algo=-1, seed=300 + i) for i in range(7)]
     env = {"MINI_NCCL_CALIBRATE": "1", "MINI_NCCL_CALIBRATE_BYTES": str(1 << 20)}
     out = _run_allreduce(n, cases, env)
     seqs = [[res["last_algo"] for res in out[r]["results"]] for r in range(n)]
     assert all(s == seqs[0] for s in seqs), seqs
     choice = out[0]["info"]["calib_choice"]
     assert choice in (0, 2), out[0]["info"]  # read, or this one-GPU communicator's scratch (ring)
-    assert seqs[0][:3] == [2, 0, 2] and seqs[0][3:] == [choice] * 3, seqs[0]
+    assert seqs[0][:4] == [2, 0, 0, 2] and seqs[0][4:] == [choice] * 3, seqs[0]
     for r in range(n):
         i = out[r]["info"]
         assert i["calib_choice"] == choice and i["calib_ms"][0] > 0 and i["calib_ms"][1] > 0, i
