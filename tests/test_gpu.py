@@ -213,6 +213,17 @@ def test_allreduce_10_ranks(dev, algo):
     _run_allreduce(10, cases, env, timeout=600)
 
 
+def test_read_schedule_8_ranks_mixed_calls(dev):
+    # the node's rank count through 20 read calls of changing size, placement and dtype on one
+    # communicator: the 16-record board wraps, small calls run a few pipelines and large ones
+    # all of them, fresh buffers bring the mapping round, reused ones skip it -- every call
+    # bit-exact against the oracle
+    sizes = [4099, 1 << 20, 77, 8 * 1000 + 5, (1 << 22) + 9, 640, 1 << 18, 123457, 8 * 64 + 3, 1 << 21]
+    cases = [_case(dtype=("f32", "bf16")[i % 2], count=sizes[i % len(sizes)], algo=2, inplace=(i % 3 == 0),
+                   seed=500 + i, vary=(i % 4 == 1), calls=1 + (i % 4 == 1)) for i in range(20)]
+    _run_allreduce(8, cases, {"GPU_MAX_HW_QUEUES": "2"}, timeout=600)
+
+
 def test_allreduce_8_ranks_c3_ring_128mib(dev):
     # C3's schedule (the reference's ring) in fp32 at 8 ranks on 128 MiB per rank: 16 MiB chunks,
     # every one of the 256 pipelines busy (64 KiB payloads), bit-exact vs the oracle
