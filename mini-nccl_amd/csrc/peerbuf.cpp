@@ -230,11 +230,10 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
   try {
     return negotiate_body(k, send, recv, eligible, count, dtype, op, sync_previous, psend, precv, vec_all, pin,
                           my_t, max_t, wait);
-  } catch (const PeerGaveUp&) {
-    throw;
   } catch (...) {
-    // this rank gives up (a peer that never came, a mapping that failed): say so on the board,
-    // so every peer waiting in a rendezvous with it fails at once instead of at its own limit
+    // this rank gives up (a peer that never came or gave up itself, a mapping that failed): say
+    // so on the board, so every peer waiting in a rendezvous with it fails at once instead of at
+    // its own limit (the abandonment cascades through the ranks)
     board_->gave_up[rank_].v.store(k, std::memory_order_release);
     throw;
   }
