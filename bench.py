@@ -484,6 +484,17 @@ def peer_topology(dev, n, same_device):
     return out
 
 
+def calibration_record(comm):
+    """MINI_NCCL_CALIBRATE (off by default): what the measured choice decided, if it ran"""
+    if os.environ.get("MINI_NCCL_CALIBRATE", "0") in ("", "0"):
+        return "off (MINI_NCCL_CALIBRATE=0, the library default)"
+    i = comm.info()
+    if i["calib_choice"] < 0:
+        return "on, undecided"
+    return {"choice": ALGO_NAMES[i["calib_choice"]], "read_ms": round(i["calib_ms"][0], 4),
+            ALGO_NAMES[i["scratch_algo"]] + "_ms": round(i["calib_ms"][1], 4)}
+
+
 def pmc_traffic(key):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/pmc_summary.json)."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -692,14 +703,16 @@ def main():
     else:
         comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
         info = comm.info()
-        # auto: the library's own choice, measured choice (MINI_NCCL_CALIBRATE) included; the
-        # schedule it ran is read back after the run
+        # the headline runs the library's default for device buffers (MINI_NCCL_ALGO=auto: the
+        # read schedule; the measured choice is off by default); --algo forces one schedule
         auto_mode = args.algo == "auto"
         if auto_mode:
             args.algo = ALGO_NAMES[info["algo"]]
+        headline_algo = args.algo
         send = torch.ones(count, device=dev, dtype=tdt)
         recv = torch.empty(count, device=dev, dtype=tdt)
         sh = stream.cuda_stream
+        sum_bytes = 3 * esz * (n - 1) * (count // n)  # the scatter-reduce sum's bytes
 
         def make_step():
             def step():
@@ -708,11 +721,18 @@ def main():
                     raise M.NcclError(rc, "ncclAllReduce")
             return step
 
+        def inject(where):
+            """MNCCL_BENCH_INJECT=<where>: rehearses the failure paths below (a GPU fault aborts the
+            process: the armed line must still come out)"""
+            if os.environ.get("MNCCL_BENCH_INJECT") == where and rank == 0:
+                log(f"injected abort at {where}")
+                os.abort()
+            if os.environ.get("MNCCL_BENCH_INJECT") == where + "_error":
+                raise M.NcclError(M.ncclInternalError, f"injected at {where} (MNCCL_BENCH_INJECT)")
+
         def run_algo(algo, auto=False):
             comm.set_algo(M.ALGO_AUTO if auto else ALGO_NAMES.index(algo))
-            inj = os.environ.get("MNCCL_BENCH_FAIL_AUTO", "")  # rehearses the recovery below:
-            if (auto and inj in ("1", "2")) or (inj == "2" and algo == "read"):  # 2: read fails too
-                raise M.NcclError(M.ncclInternalError, "injected (MNCCL_BENCH_FAIL_AUTO)")
+            inject(f"run_{algo}")
             step = make_step()
             recv.fill_(-1.0)
             for _ in range(max(1, args.warmup)):
@@ -726,20 +746,109 @@ def main():
             ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream,
                                     barrier=dist.barrier)
             i = comm.info()
-            if auto:  # the measured choice when decided, else the default read
-                ok = ok and i["last_algo"] == (i["calib_choice"] if i["calib_choice"] >= 0 else ALGO_NAMES.index("read"))
-            else:
-                ok = ok and i["last_algo"] == ALGO_NAMES.index(algo)  # no fallback happened
+            want = ALGO_NAMES.index(algo)
+            if auto and i["calib_choice"] >= 0:  # MINI_NCCL_CALIBRATE=1: the measured choice
+                want = i["calib_choice"]
+            ok = ok and i["last_algo"] == want  # the timed calls ran this schedule (no fallback)
             send.fill_(1.0)
             ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
             return max_over_ranks(wall), max_over_ranks(ev_ms), ok
 
-        # the xGMI roofline the schedules are bound by: write bandwidth per link with the hot
-        # path's store form, one link per rank (the ring's) and every link at once (direct's)
+        def point(algo, wall, ev_ms, ok):
+            """one schedule's measured line: algbw, its kernel's roofline fraction (SURVEY s8(d)
+            sum bytes over the fused kernel's own time) and every byte it moves through HBM"""
+            ms_ = wall / args.steps * 1e3
+            fused = fused_bytes(algo, esz, count // n, n)
+            return {"algo": algo, "value": round(nbytes / (ms_ / 1e3) / 1e9, 3), "ms_per_step": round(ms_, 4),
+                    "kernel_ms": round(ev_ms, 4), "result_check": "ok" if ok else "FAILED",
+                    "roofline": {"frac": round(sum_bytes / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "fused_frac": round(fused / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "fused_alg_bytes_per_launch": fused}}
+
+        # 1. the headline, before any probe or other schedule: once it is measured, the line is
+        # armed, so a fault in anything after it still leaves the line on stdout
+        headline_error = None
+        try:
+            wall, ev_ms, ok = run_algo(headline_algo, auto=auto_mode)
+        except M.NcclError as e:
+            # the default schedule failed (every rank's calls fail alike): the line says so
+            # (result_check FAILED, headline_error) and carries the ring's number, measured on a
+            # new communicator, so the failure is on record with a measured fallback beside it
+            headline_error = f"{headline_algo}: {str(e)[:200]}"
+            log(f"headline failed ({e}); new communicator, ring schedule")
+            try:
+                comm.destroy()
+            except Exception:
+                pass
+            torch.cuda.synchronize()
+            dist.barrier()
+            comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
+            auto_mode = False
+            args.algo = "ring"
+            wall, ev_ms, ok = run_algo("ring")
+            ok = False
+        ms = wall / args.steps * 1e3
+        algbw = nbytes / (ms / 1e3) / 1e9
+        alg_bytes = sum_bytes
+        result.update({
+            "value": round(algbw, 3),
+            "ms_per_step": round(ms, 4),
+            "config": {"workload": f"{n}-rank all-reduce (reference ring association), 1 GiB {args.dtype} per rank, "
+                                   f"HIP IPC over xGMI, {args.algo} schedule",
+                       "count": count, "bytes": nbytes, "algo": args.algo, "slice_bytes": info["slice_bytes"],
+                       "channels": info["channels"], "slots": info["slots"], "threads": info["threads"],
+                       "pipelines": info["pipelines"], "scratch_bytes": info["scratch_bytes"],
+                       "ranks_on_device": info["ranks_on_device"],
+                       "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
+                       "headline_schedule": ("the library default for device buffers (MINI_NCCL_ALGO=auto -> read: each "
+                                             "rank folds its chunk from the peers' send buffers over the links in the "
+                                             "reference ring's association order, then loads the peers' results -- the "
+                                             "same bits as the ring, 2/n of the buffer per link instead of 2(n-1)/n "
+                                             "through one link); the north star's ring is measured beside it in "
+                                             "schedules.ring with its own roofline and link fractions"
+                                             if headline_algo == "read" else f"{headline_algo} (forced by --algo)"),
+                       "calibration": calibration_record(comm)},
+            "busbw": round(algbw * 2 * (n - 1) / n, 3),
+            "schedules": {args.algo: point(args.algo, wall, ev_ms, ok)},
+        })
+        if headline_error:
+            result["config"]["headline_error"] = headline_error
+            result["config"]["result_check"] = f"FAILED: the default schedule failed ({headline_error}); value is the ring's"
+        fused = fused_bytes(args.algo, esz, count // n, n)
+        fa = fused / (ev_ms / 1e3) / 1e9
+        result["roofline"] = {"bound": "hbm", "achieved": round(alg_bytes / (ev_ms / 1e3) / 1e9, 2),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(alg_bytes / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "traffic": None, "kernel": f"{args.algo}_kernel", "kernel_ms": round(ev_ms, 4),
+                              "alg_bytes_per_launch": alg_bytes, "fused_alg_bytes_per_launch": fused,
+                              "fused_achieved": round(fa, 2), "fused_frac": round(fa / HBM_PEAK_GBS, 4)}
+        # the host path beside every N (SURVEY s8d): the CPU ring, timed before the GPU was touched
+        result["cpu_baseline"] = cpu_ring
+        if rank == 0:
+            arm(result)
+        # 2. the other schedules on the same buffers (same bits): the ring first -- C3 names it
+        # ("8 MI355X ring"), the north star keeps it unchanged -- each its own labelled point
+        if not args.no_alt:
+            for other in ("ring", "direct", "read"):
+                if other in result["schedules"]:
+                    continue
+                if rank == 0:
+                    log(f"schedule {other}")
+                try:
+                    result["schedules"][other] = point(other, *run_algo(other))
+                except Exception as e:
+                    result["schedules"][other] = {"algo": other, "error": str(e)[:200]}
+                if rank == 0:
+                    arm(result)
+            comm.set_algo(M.ALGO_AUTO if auto_mode else ALGO_NAMES.index(args.algo))
+        # 3. the xGMI roofline the schedules are bound by, after the schedules themselves: bytes
+        # per link with the hot path's access forms, one link per rank (the ring's) and every link
+        # at once (direct's stores, read's loads)
         link = {}
         try:
             torch.cuda.synchronize()
             dist.barrier()
+            inject("probe")
             # min over ranks (the ceiling is set by the slowest link); max alongside for the spread
             pn = comm.link_probe(False, 0, 10)
             pm = comm.link_probe(True, 0, 10)
@@ -747,8 +856,6 @@ def main():
             link["probe_mesh_GBps_per_link"] = round(max_over_ranks(-pm) * -1, 2)
             link["probe_next_max_GBps"] = round(max_over_ranks(pn), 2)
             link["probe_mesh_max_GBps_per_link"] = round(max_over_ranks(pm), 2)
-            # other access forms over the same links (min over ranks), for the choice of form
-            # only: push non-temporal / default policy, pull (loads over the link)
             var = {}
             # *_user: the peers' ordinary device memory (hipMalloc, what the read schedule loads
             # from) instead of their uncached scratch
@@ -766,117 +873,37 @@ def main():
                 link["topology_rank0"] = peer_topology(local_rank, n, args.same_device)
             except Exception as e:
                 link["topology_rank0"] = {"error": str(e)[:120]}
-        calib = None
-        try:
-            wall, ev_ms, ok = run_algo(args.algo, auto=auto_mode)
-        except M.NcclError as e:
-            # the measured choice times the scratch schedule during the warm-up; should that (or
-            # anything else in the auto run) kill the communicator -- every rank's calls fail
-            # alike, by the first timed step at the latest -- the line is still measured: a new
-            # communicator with the read schedule explicitly (the failure is on record)
-            if not auto_mode:
-                raise
-            calib = {"error": str(e)[:200]}
-            os.environ["MINI_NCCL_CALIBRATE"] = "0"
-            auto_mode, last = False, e
-            # read first; should the read schedule itself be what fails, the scratch schedule
-            for alg in ("read", ALGO_NAMES[info["scratch_algo"]]):
-                log(f"headline failed ({last}); new communicator, {alg} schedule")
-                try:
-                    comm.destroy()
-                except Exception:
-                    pass
-                torch.cuda.synchronize()
-                dist.barrier()
-                comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
-                args.algo = alg
-                try:
-                    wall, ev_ms, ok = run_algo(alg)
-                    calib["fallback"] = f"{alg} schedule on a new communicator"
-                    break
-                except M.NcclError as e2:
-                    calib[f"{alg}_error"] = str(e2)[:200]
-                    last = e2
-            else:
-                raise last
-        if auto_mode:
-            i = comm.info()
-            args.algo = ALGO_NAMES[i["last_algo"]]  # what the timed calls ran
-            calib = ({"choice": ALGO_NAMES[i["calib_choice"]], "read_ms": round(i["calib_ms"][0], 4),
-                      ALGO_NAMES[i["scratch_algo"]] + "_ms": round(i["calib_ms"][1], 4),
-                      "rule": "MINI_NCCL_CALIBRATE: large auto calls 0-1 warm read and the scratch schedule up, "
-                              "2-3 time the scratch schedule and read; every rank's timings travel with its call "
-                              "records; later large calls run the scratch schedule only if it is >= 3 % faster "
-                              "(max over ranks)"}
-                     if i["calib_choice"] >= 0 else "off or undecided")
-        ms = wall / args.steps * 1e3
-        algbw = nbytes / (ms / 1e3) / 1e9
-        alg_bytes = 3 * esz * (n - 1) * (count // n)
-        result.update({
-            "value": round(algbw, 3),
-            "ms_per_step": round(ms, 4),
-            "config": {"workload": f"{n}-rank all-reduce (reference ring association), 1 GiB {args.dtype} per rank, "
-                                   f"HIP IPC over xGMI, {args.algo} schedule",
-                       "count": count, "bytes": nbytes, "algo": args.algo, "slice_bytes": info["slice_bytes"],
-                       "channels": info["channels"], "slots": info["slots"], "threads": info["threads"],
-                       "pipelines": info["pipelines"], "scratch_bytes": info["scratch_bytes"],
-                       "ranks_on_device": info["ranks_on_device"],
-                       "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
-                       "algo_rule": "MINI_NCCL_ALGO=auto: read (peers' buffers loaded over the links, no scratch) "
-                                    "for device buffers; otherwise direct from 3 ranks on more than one GPU, else "
-                                    "ring (no all-reduce at init)",
-                       "calibration": calib},
-            "busbw": round(algbw * 2 * (n - 1) / n, 3),
-        })
-        # ceiling of each schedule from the probed links (min over ranks): ring moves
-        # 2(n-1)/n of the buffer through one link, direct 2/n through each of n-1 links
-        # read moves the same 2/n through each link as direct, as loads (the probe's mesh pull)
+        # each schedule's ceiling from the probed links (min over ranks): the ring moves
+        # 2(n-1)/n of the buffer through one link, direct 2/n through each of n-1 links as
+        # stores, read the same 2/n per link as loads (the probe's mesh pull from user memory)
         if "probe_next_GBps" in link:
-            ring_ceiling = link["probe_next_GBps"] * n / (2 * (n - 1))
-            direct_ceiling = link["probe_mesh_GBps_per_link"] * n / 2
-            link.update({"ring_ceiling_GBps": round(ring_ceiling, 2), "direct_ceiling_GBps": round(direct_ceiling, 2)})
-            ceiling = direct_ceiling if args.algo == "direct" else ring_ceiling
             pv = link.get("probe_variants_GBps_per_link", {})
-            pull = pv.get("mesh_pull_sys_user") or pv.get("mesh_pull_sys")  # read loads user buffers
+            pull = pv.get("mesh_pull_sys_user") or pv.get("mesh_pull_sys")
+            ceil = {"ring": link["probe_next_GBps"] * n / (2 * (n - 1)),
+                    "direct": link["probe_mesh_GBps_per_link"] * n / 2}
             if pull:
-                link["read_ceiling_GBps"] = round(pull * n / 2, 2)
-                if args.algo == "read":
-                    ceiling = pull * n / 2
-            link["frac"] = round(algbw / ceiling, 4)
+                ceil["read"] = pull * n / 2
+            link.update({f"{a}_ceiling_GBps": round(c, 2) for a, c in ceil.items()})
+            for a, ptn in result["schedules"].items():
+                if a in ceil and "value" in ptn:
+                    ptn["link_frac"] = round(ptn["value"] / ceil[a], 4)
+            if args.algo in ceil:
+                link["frac"] = round(algbw / ceil[args.algo], 4)
         result["link"] = link
         if rank == 0:
             arm(result)
-        if not args.no_alt:
-            # the other schedules on the same buffers (same bits), for comparison
-            result["alt"] = []
-            for other in (a for a in ALGO_NAMES if a != args.algo):
-                try:
-                    w2, e2, ok2 = run_algo(other)
-                    ms2 = w2 / args.steps * 1e3
-                    result["alt"].append({"algo": other, "value": round(nbytes / (ms2 / 1e3) / 1e9, 3),
-                                          "ms_per_step": round(ms2, 4), "kernel_ms": round(e2, 4),
-                                          "result_check": "ok" if ok2 else "FAILED"})
-                except Exception as e:
-                    result["alt"].append({"algo": other, "error": str(e)[:200]})
-                if rank == 0:
-                    arm(result)
-            comm.set_algo(M.ALGO_AUTO if auto_mode else ALGO_NAMES.index(args.algo))
-        # rank 0's kernel, measured where this run runs (ranks sharing one GPU: the proxy entry)
         traffic, tsrc = pmc_traffic(f"{args.algo}_{args.dtype}_1GiB_n{n}" + ("_same_gpu" if args.same_device else ""))
+        if traffic is not None:
+            result["roofline"].update({"traffic": traffic, "traffic_source": tsrc})
         kern_key = f"{args.algo}_kernel"
-    achieved = alg_bytes / (ev_ms / 1e3) / 1e9
-    result["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                          "kernel": kern_key, "kernel_ms": round(ev_ms, 4), "alg_bytes_per_launch": alg_bytes}
-    if traffic is not None:
-        result["roofline"]["traffic_source"] = tsrc
+    if n == 1:
+        achieved = alg_bytes / (ev_ms / 1e3) / 1e9
+        result["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                              "kernel": kern_key, "kernel_ms": round(ev_ms, 4), "alg_bytes_per_launch": alg_bytes}
+        if traffic is not None:
+            result["roofline"]["traffic_source"] = tsrc
     if n > 1:
-        # `achieved` counts SURVEY.md §8(d)'s sum-kernel bytes only; the fused kernel also does
-        # the raw send and the all-gather (fused_bytes: every byte through this rank's HBM)
-        fused = fused_bytes(args.algo, esz, count // n, n)
-        fa = fused / (ev_ms / 1e3) / 1e9
-        result["roofline"].update({"fused_alg_bytes_per_launch": fused, "fused_achieved": round(fa, 2),
-                                   "fused_frac": round(fa / HBM_PEAK_GBS, 4)})
         # roofline.frac above is SURVEY §8(d)'s sum bytes over the FUSED all-reduce kernel's time.
         # For reference only: the same element-wise op as a standalone launch on THIS GPU over the
         # (n-1) * chunk elements a rank reduces per call (same bytes), HIP events around each
@@ -923,9 +950,10 @@ def main():
             result["host_inclusive"] = host_inclusive_n1(M, torch, dev, count, tdt, ndt)
         except Exception as e:
             result["host_inclusive"] = {"error": str(e)[:200]}
-    result["cpu_baseline"] = cpu
-    if cpu_ring is not None:
-        result["cpu_ring_baseline"] = cpu_ring
+    if n == 1:
+        result["cpu_baseline"] = cpu
+    elif cpu_ring is not None:
+        result["cpu_ring_baseline"] = cpu_ring  # the same object as cpu_baseline (kept under its old name)
     if rank == 0:
         arm(result)
     guard = None

@@ -77,8 +77,8 @@ Config Config::from_env() {
   if (tb < (1LL << 20)) tb = 1LL << 20;
   c.tune_bytes = (size_t)(tb & ~255LL);
   c.stage_host = env_int("MINI_NCCL_STAGE_HOST", 0) != 0;
-  if (const char* cal = std::getenv("MINI_NCCL_CALIBRATE"); cal && *cal && strcmp(cal, "auto") != 0)
-    c.calibrate = env_int("MINI_NCCL_CALIBRATE", -1) != 0 ? 1 : 0;
+  if (const char* cal = std::getenv("MINI_NCCL_CALIBRATE"); cal && *cal)
+    c.calibrate = strcmp(cal, "auto") == 0 ? -1 : env_int("MINI_NCCL_CALIBRATE", 0) != 0 ? 1 : 0;
   long long cb = env_int("MINI_NCCL_CALIBRATE_BYTES", 64LL << 20);
   c.calibrate_bytes = (size_t)(cb < 1 ? 1 : cb);
   c.timeout_ms = (double)env_int("MINI_NCCL_TIMEOUT_MS", 10000);

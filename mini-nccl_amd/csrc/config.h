@@ -27,8 +27,9 @@ struct Config {
   int tune = 0;                    // MINI_NCCL_TUNE   1: auto algo times both schedules at init (n >= 3)
   size_t tune_bytes = 64u << 20;   // MINI_NCCL_TUNE_BYTES per-rank buffer of that calibration
   int stage_host = 0;              // MINI_NCCL_STAGE_HOST pinned host buffers: 0 = kernel maps them, 1 = staged copy
-  int calibrate = -1;              // MINI_NCCL_CALIBRATE auto algo: time read vs the scratch schedule on the first
-                                   //   large calls and keep the faster; -1 = when the ranks span >1 GPU, 0 off, 1 on
+  int calibrate = 0;               // MINI_NCCL_CALIBRATE auto algo: time read vs the scratch schedule on the first
+                                   //   large calls and keep the faster; 0 off (default: the scratch schedule has not
+                                   //   yet run across GPUs), 1 on, "auto" = when the ranks span >1 GPU
   size_t calibrate_bytes = 64u << 20;  // MINI_NCCL_CALIBRATE_BYTES calls at least this large are timed / switched
   double timeout_ms = 10000.0;     // MINI_NCCL_TIMEOUT_MS (reference watchdog: 10 s)
   int port = 8888;                 // MINI_NCCL_PORT   bootstrap port (reference: 8888)
