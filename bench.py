@@ -218,7 +218,9 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-        torch.cuda.empty_cache()
+        # no torch.cuda.empty_cache(): the next point's tensors come from the same cached segments,
+        # so the read schedule shares allocations it shared before (a segment handed back to HIP
+        # and re-allocated at the same address would not be shared again, csrc/ipcreg.h)
 
 
 def verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream, calls=3, barrier=None):
@@ -765,16 +767,77 @@ def main():
                                  "fused_frac": round(fused / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                                  "fused_alg_bytes_per_launch": fused}}
 
-        # 1. the headline, before any probe or other schedule: once it is measured, the line is
-        # armed, so a fault in anything after it still leaves the line on stdout
-        headline_error = None
+        def set_line(algo, wall, ev_ms, ok, note=None):
+            """the line's headline fields from one schedule's measurement"""
+            ms_ = wall / args.steps * 1e3
+            bw = nbytes / (ms_ / 1e3) / 1e9
+            fused = fused_bytes(algo, esz, count // n, n)
+            fa = fused / (ev_ms / 1e3) / 1e9
+            result.update({
+                "value": round(bw, 3),
+                "ms_per_step": round(ms_, 4),
+                "busbw": round(bw * 2 * (n - 1) / n, 3),
+                "config": {"workload": f"{n}-rank all-reduce (reference ring association), 1 GiB {args.dtype} per "
+                                       f"rank, HIP IPC over xGMI, {algo} schedule",
+                           "count": count, "bytes": nbytes, "algo": algo, "slice_bytes": info["slice_bytes"],
+                           "channels": info["channels"], "slots": info["slots"], "threads": info["threads"],
+                           "pipelines": info["pipelines"], "scratch_bytes": info["scratch_bytes"],
+                           "ranks_on_device": info["ranks_on_device"],
+                           "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
+                           "headline_schedule": headline_why, "calibration": calibration_record(comm)},
+                "roofline": {"bound": "hbm", "achieved": round(sum_bytes / (ev_ms / 1e3) / 1e9, 2),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(sum_bytes / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "traffic": None, "kernel": f"{algo}_kernel", "kernel_ms": round(ev_ms, 4),
+                             "alg_bytes_per_launch": sum_bytes, "fused_alg_bytes_per_launch": fused,
+                             "fused_achieved": round(fa, 2), "fused_frac": round(fa / HBM_PEAK_GBS, 4)},
+                # the host path beside every N (SURVEY s8d): the CPU ring, timed before the GPU was
+                # touched
+                "cpu_baseline": cpu_ring,
+            })
+            if note:
+                result["config"]["result_check"] = note
+            return bw
+
+        headline_why = ("the library default for device buffers (MINI_NCCL_ALGO=auto -> read: each rank folds its "
+                        "chunk from the peers' send buffers over the links in the reference ring's association "
+                        "order, then loads the peers' results -- the same bits as the ring, 2/n of the buffer per "
+                        "link instead of 2(n-1)/n through one link); the north star's ring is measured first and "
+                        "beside it in schedules.ring with its own roofline and link fractions"
+                        if headline_algo == "read" else f"{headline_algo} ({'forced by --algo' if not auto_mode else 'auto'})")
+        # 0. a line exists before anything runs on the GPU: if the process dies (a GPU fault
+        # aborts it), the armed line is printed
+        result.update({"value": 0.0, "cpu_baseline": cpu_ring,
+                       "error": "the process died before any schedule was measured"})
+        if rank == 0:
+            arm(result)
+        result.pop("error")
+        result["schedules"] = {}
+        # 1. the reference's ring first (the north star's schedule, C3's "8 MI355X ring"): measured
+        # and armed before the default, so a fault in the default still leaves a measured line
+        if headline_algo != "ring":
+            if rank == 0:
+                log("schedule ring (armed first)")
+            try:
+                wr, er, okr = run_algo("ring")
+                result["schedules"]["ring"] = point("ring", wr, er, okr)
+                set_line("ring", wr, er, okr, note=f"PROVISIONAL: the ring's line; the default schedule "
+                                                   f"({headline_algo}) was being measured when the process ended")
+                if rank == 0:
+                    arm(result)
+            except M.NcclError as e:
+                result["schedules"]["ring"] = {"algo": "ring", "error": str(e)[:200]}
+        # 2. the headline: the library default (or --algo)
         try:
             wall, ev_ms, ok = run_algo(headline_algo, auto=auto_mode)
+            result["schedules"][headline_algo] = point(headline_algo, wall, ev_ms, ok)
+            algbw = set_line(headline_algo, wall, ev_ms, ok)
         except M.NcclError as e:
             # the default schedule failed (every rank's calls fail alike): the line says so
             # (result_check FAILED, headline_error) and carries the ring's number, measured on a
             # new communicator, so the failure is on record with a measured fallback beside it
             headline_error = f"{headline_algo}: {str(e)[:200]}"
+            result["schedules"][headline_algo] = {"algo": headline_algo, "error": headline_error}
             log(f"headline failed ({e}); new communicator, ring schedule")
             try:
                 comm.destroy()
@@ -786,48 +849,14 @@ def main():
             auto_mode = False
             args.algo = "ring"
             wall, ev_ms, ok = run_algo("ring")
-            ok = False
-        ms = wall / args.steps * 1e3
-        algbw = nbytes / (ms / 1e3) / 1e9
-        alg_bytes = sum_bytes
-        result.update({
-            "value": round(algbw, 3),
-            "ms_per_step": round(ms, 4),
-            "config": {"workload": f"{n}-rank all-reduce (reference ring association), 1 GiB {args.dtype} per rank, "
-                                   f"HIP IPC over xGMI, {args.algo} schedule",
-                       "count": count, "bytes": nbytes, "algo": args.algo, "slice_bytes": info["slice_bytes"],
-                       "channels": info["channels"], "slots": info["slots"], "threads": info["threads"],
-                       "pipelines": info["pipelines"], "scratch_bytes": info["scratch_bytes"],
-                       "ranks_on_device": info["ranks_on_device"],
-                       "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
-                       "headline_schedule": ("the library default for device buffers (MINI_NCCL_ALGO=auto -> read: each "
-                                             "rank folds its chunk from the peers' send buffers over the links in the "
-                                             "reference ring's association order, then loads the peers' results -- the "
-                                             "same bits as the ring, 2/n of the buffer per link instead of 2(n-1)/n "
-                                             "through one link); the north star's ring is measured beside it in "
-                                             "schedules.ring with its own roofline and link fractions"
-                                             if headline_algo == "read" else f"{headline_algo} (forced by --algo)"),
-                       "calibration": calibration_record(comm)},
-            "busbw": round(algbw * 2 * (n - 1) / n, 3),
-            "schedules": {args.algo: point(args.algo, wall, ev_ms, ok)},
-        })
-        if headline_error:
+            algbw = set_line("ring", wall, ev_ms, False,
+                             note=f"FAILED: the default schedule failed ({headline_error}); value is the ring's")
             result["config"]["headline_error"] = headline_error
-            result["config"]["result_check"] = f"FAILED: the default schedule failed ({headline_error}); value is the ring's"
-        fused = fused_bytes(args.algo, esz, count // n, n)
-        fa = fused / (ev_ms / 1e3) / 1e9
-        result["roofline"] = {"bound": "hbm", "achieved": round(alg_bytes / (ev_ms / 1e3) / 1e9, 2),
-                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": round(alg_bytes / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                              "traffic": None, "kernel": f"{args.algo}_kernel", "kernel_ms": round(ev_ms, 4),
-                              "alg_bytes_per_launch": alg_bytes, "fused_alg_bytes_per_launch": fused,
-                              "fused_achieved": round(fa, 2), "fused_frac": round(fa / HBM_PEAK_GBS, 4)}
-        # the host path beside every N: the CPU ring, timed before the GPU was touched
-        result["cpu_baseline"] = cpu_ring
+        else:
+            args.algo = headline_algo
         if rank == 0:
             arm(result)
-        # 2. the other schedules on the same buffers (same bits): the ring first -- C3 names it
-        # ("8 MI355X ring"), the north star keeps it unchanged -- each its own labelled point
+        # 3. the other schedules on the same buffers (same bits), each its own labelled point
         if not args.no_alt:
             for other in ("ring", "direct", "read"):
                 if other in result["schedules"]:
@@ -841,7 +870,7 @@ def main():
                 if rank == 0:
                     arm(result)
             comm.set_algo(M.ALGO_AUTO if auto_mode else ALGO_NAMES.index(args.algo))
-        # 3. the xGMI roofline the schedules are bound by, after the schedules themselves: bytes
+        # 4. the xGMI roofline the schedules are bound by, after the schedules themselves: bytes
         # per link with the hot path's access forms, one link per rank (the ring's) and every link
         # at once (direct's stores, read's loads)
         link = {}
@@ -1019,8 +1048,7 @@ def main():
                 arm(result)
     if n > 1:
         comm.destroy()
-        del send, recv
-        torch.cuda.empty_cache()
+        del send, recv  # back to torch's cache (not to HIP: see sweep_point)
         if not args.no_sweep and args.dtype == "f32":
             t_sw = time.time()
             result["sweep"] = {}

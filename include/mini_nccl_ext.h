@@ -11,7 +11,9 @@
  *   mncclCommGetAsyncError  sticky error of a communicator (a timed-out or aborted
  *                        all-reduce leaves the ring state inconsistent; every later
  *                        call returns this error), like NCCL's ncclCommGetAsyncError.
- *   mncclCommGetInfo     resolved configuration of a communicator.
+ *   mncclCommGetInfo     resolved configuration of a communicator (mncclCommGetInfoV: the
+ *                        caller states its struct's size, so an older caller is never
+ *                        written past its end).
  *   mncclCommSetAlgo     choose the schedule for later calls (same association order).
  *   mncclCommLinkProbe   measure the xGMI write bandwidth the schedules are bound by.
  */
@@ -24,12 +26,15 @@
 extern "C" {
 #endif
 
+/* mncclVersion() of the library this header describes; mncclCommInfo_t grew in 300 */
+#define MNCCL_VERSION 300
+
 /* schedules; all produce bit-identical results (same fold order per element) */
 typedef enum {
-  mncclAlgoAuto = -1,  /* the library's default: read for device buffers; with
-                          MINI_NCCL_CALIBRATE (on by default when the ranks span more than one
-                          GPU) the first calls of at least MINI_NCCL_CALIBRATE_BYTES time read
-                          against the scratch schedule and later such calls run the faster */
+  mncclAlgoAuto = -1,  /* the library's default: read for device buffers it can share; with
+                          MINI_NCCL_CALIBRATE=1 (off by default) the first calls of at least
+                          MINI_NCCL_CALIBRATE_BYTES time read against the scratch schedule and
+                          later such calls run the faster */
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
   mncclAlgoDirect = 1, /* every peer pushes its slice of chunk c straight to rank c over its
                           own xGMI link; c folds them in ring order c, c+1, ..., c-1 and
@@ -39,8 +44,9 @@ typedef enum {
                           their send buffers (mapped per allocation, negotiated per call),
                           folds them in the same order into its recv, and every peer loads
                           the result from there; a call whose buffers some rank cannot share
-                          (host memory) runs the scratch schedule instead, on every rank
-                          alike */
+                          (host memory; an allocation at an address the process exported
+                          before, see csrc/ipcreg.h) runs the scratch schedule instead, on
+                          every rank alike */
 } mncclAlgo_t;
 
 typedef struct {
@@ -66,13 +72,20 @@ typedef struct {
   int last_algo;          /* schedule the last all-reduce ran (mncclAlgo_t; -1: no kernel
                              yet): mncclAlgoRead falls back to the scratch schedule for a
                              call some rank's buffers cannot take part in */
-  size_t peer_mappings;   /* read schedule: peer allocations mapped into this process */
+  size_t peer_mappings;   /* peer allocations mapped into this process (scratch, mailboxes and
+                             read-schedule buffers of every communicator; csrc/ipcreg.h) */
   int scratch_algo;       /* the read schedule's fallback (ring or direct), chosen from the
                              ranks' GPUs: direct from 3 ranks on more than one GPU */
   int calib_choice;       /* MINI_NCCL_CALIBRATE: schedule kept for large calls (mncclAlgo_t), -1
                              while undecided or when calibration is off */
   double calib_ms[2];     /* the timings it was decided on: read, scratch schedule (ms per call,
                              max over ranks); 0 until decided */
+  /* since 300 */
+  unsigned long long ipc_open_failures;  /* hipIpcOpenMemHandle failures in this process */
+  unsigned long long read_map_failures;  /* read calls this rank could not map (call fell back) */
+  unsigned long long read_rounds;        /* read calls that needed the mapping round */
+  unsigned long long closed_freed;       /* imports closed because their owner freed them */
+  size_t live_exports;                   /* this process's user allocations exported and alive */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,
@@ -81,6 +94,9 @@ ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming
 ncclResult_t mncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError);
 
 ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info);
+/* writes min(size, sizeof(mncclCommInfo_t)) bytes: callers built against an older header pass
+   their struct's size */
+ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* info, size_t size);
 
 /* every rank must make the same choice before its next all-reduce; mncclAlgoAuto restores the
    default (and its calibration) */

@@ -13,7 +13,10 @@
 #include <stdexcept>
 #include <string>
 
+#include <cstring>
+
 #include "comm.h"
+#include "ipcreg.h"
 #include "kernels.h"
 #include "mini_nccl_api.h"
 #include "mini_nccl_ext.h"
@@ -138,9 +141,16 @@ ncclResult_t mncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError) {
 }
 
 ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info) {
-  if (!comm || !info) return ncclInvalidArgument;
+  return mncclCommGetInfoV(comm, info, sizeof(mncclCommInfo_t));
+}
+
+ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
+  if (!comm || !out) return ncclInvalidArgument;
   const Comm* c = reinterpret_cast<const Comm*>(comm);
   const mnccl::Config& k = c->config();
+  mncclCommInfo_t full;
+  memset(&full, 0, sizeof full);
+  mncclCommInfo_t* info = &full;
   info->rank = c->rank();
   info->nranks = c->nranks();
   info->device = c->device();
@@ -166,6 +176,12 @@ ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info) {
   info->calib_choice = c->calib_choice();
   info->calib_ms[0] = c->calib_ms(0);
   info->calib_ms[1] = c->calib_ms(1);
+  info->ipc_open_failures = mnccl::ipc::open_failures();
+  info->read_map_failures = c->peer_buffers().map_failures();
+  info->read_rounds = c->peer_buffers().agreements();
+  info->closed_freed = c->peer_buffers().closed_freed();
+  info->live_exports = mnccl::ipc::live_exports();
+  memcpy(out, &full, size < sizeof full ? size : sizeof full);
   return ncclSuccess;
 }
 
@@ -191,6 +207,6 @@ ncclResult_t mncclCommLinkProbe(ncclComm_t comm, int allPeers, size_t bytes, int
   }
 }
 
-int mncclVersion(void) { return 100; /* 0.1.0 */ }
+int mncclVersion(void) { return MNCCL_VERSION; /* 0.3.0: mncclCommInfo_t grew, mncclCommGetInfoV */ }
 
 }  // extern "C"

@@ -14,6 +14,7 @@
 #include <random>
 #include <stdexcept>
 
+#include "ipcreg.h"
 #include "schedule.h"
 
 namespace mnccl {
@@ -102,9 +103,10 @@ struct PeerInfo {
   int32_t depth, overlap, pull, calibrate;
   uint64_t calibrate_bytes;
   hipIpcMemHandle_t scratch_h, mbox_h;
-  uint64_t scratch_ptr, mbox_ptr;  // raw addresses for ranks living in the same process
+  uint64_t scratch_ptr, mbox_ptr;  // raw addresses (same-process ranks) / the allocations' bases
+  uint64_t scratch_id, mbox_id;    // HIP allocation ids (the import registry's keys)
 };
-constexpr uint32_t kInfoMagic = 0x4d4e4932u;  // 'MNI2'
+constexpr uint32_t kInfoMagic = 0x4d4e4933u;  // 'MNI3'
 
 }  // namespace
 
@@ -146,8 +148,10 @@ void Comm::setup_device_resources() {
   hip_check(hipHostGetDevicePointer((void**)&d_ctl_, h_ctl_, 0), "ctl device pointer");
   hip_check(hipEventCreateWithFlags(&order_ev_, hipEventDisableTiming), "event");
   if (nranks_ > 1) {
-    hip_check(hipExtMallocWithFlags((void**)&scratch_, scratch_bytes_, hipDeviceMallocUncached), "alloc scratch");
-    hip_check(hipExtMallocWithFlags((void**)&mbox_, mbox_bytes_, hipDeviceMallocUncached), "alloc mailbox");
+    // from the process's pool (ipcreg.h): a communicator created after another one re-uses its
+    // blocks and the peers' imports of them instead of exporting a re-used address
+    scratch_ = (char*)ipc::pool_acquire(scratch_bytes_, hipDeviceMallocUncached, &scratch_h_, &scratch_id_);
+    mbox_ = (uint64_t*)ipc::pool_acquire(mbox_bytes_, hipDeviceMallocUncached, &mbox_h_, &mbox_id_);
     const size_t seq_bytes = (size_t)2 * nranks_ * C * sizeof(uint64_t);  // C = wave channels
     hip_check(hipMalloc((void**)&pair_seq_, seq_bytes), "alloc pair_seq");
     // zeroed on a private stream: a device-wide sync (or the legacy null stream) would also wait
@@ -166,7 +170,6 @@ void Comm::setup_device_resources() {
 void Comm::exchange_and_map() {
   peer_scratch_.assign((size_t)nranks_, nullptr);
   peer_mbox_.assign((size_t)nranks_, nullptr);
-  peer_opened_.assign((size_t)nranks_, false);
   if (nranks_ == 1) return;
   PeerInfo me;
   memset(&me, 0, sizeof me);
@@ -197,10 +200,12 @@ void Comm::exchange_and_map() {
   me.pull = cfg_.pull;
   me.calibrate = cfg_.calibrate;
   me.calibrate_bytes = cfg_.calibrate_bytes;
-  hip_check(hipIpcGetMemHandle(&me.scratch_h, scratch_), "ipc handle scratch");
-  hip_check(hipIpcGetMemHandle(&me.mbox_h, mbox_), "ipc handle mailbox");
+  me.scratch_h = scratch_h_;
+  me.mbox_h = mbox_h_;
   me.scratch_ptr = (uint64_t)(uintptr_t)scratch_;
   me.mbox_ptr = (uint64_t)(uintptr_t)mbox_;
+  me.scratch_id = scratch_id_;
+  me.mbox_id = mbox_id_;
 
   std::vector<PeerInfo> all((size_t)nranks_);
   boot_.allgather(&me, all.data(), sizeof me);
@@ -280,13 +285,15 @@ void Comm::exchange_and_map() {
     // otherwise the IPC mapping's lazy peer access does it
     const int pd = local_device_with_pci(p.pci);
     if (pd >= 0 && pd != device_) enable_peer_access(device_, pd, false);
-    void* ps = nullptr;
-    void* pm = nullptr;
-    hip_check(hipIpcOpenMemHandle(&ps, p.scratch_h, hipIpcMemLazyEnablePeerAccess), "ipc open scratch");
-    hip_check(hipIpcOpenMemHandle(&pm, p.mbox_h, hipIpcMemLazyEnablePeerAccess), "ipc open mailbox");
-    peer_scratch_[(size_t)q] = (char*)ps;
+    // through the process's import registry: a peer block this process imported for an earlier
+    // communicator is still mapped (imports of pool blocks are never closed, ipcreg.h)
+    hipError_t e = hipSuccess;
+    char* ps = ipc::open_import(p.nonce, p.scratch_ptr, p.scratch_id, p.scratch_h, &e);
+    hip_check(ps ? hipSuccess : e, "ipc open scratch");
+    char* pm = ipc::open_import(p.nonce, p.mbox_ptr, p.mbox_id, p.mbox_h, &e);
+    hip_check(pm ? hipSuccess : e, "ipc open mailbox");
+    peer_scratch_[(size_t)q] = ps;
     peer_mbox_[(size_t)q] = (uint64_t*)pm;
-    peer_opened_[(size_t)q] = true;
   }
   // every rank has mapped every peer and its own memory is zeroed before anyone writes
   boot_.barrier();
@@ -354,19 +361,9 @@ Comm::~Comm() {
   if (have_last_ && order_ev_) hipEventSynchronize(order_ev_);
   if (nranks_ > 1 && !peer_scratch_.empty()) {
     try {
-      if (sticky_ == ncclSuccess) boot_.barrier();  // nobody still writes into my memory
-    } catch (...) {
-    }
-    for (int q = 0; q < nranks_; ++q) {
-      if (peer_opened_[(size_t)q]) {
-        hipIpcCloseMemHandle(peer_scratch_[(size_t)q]);
-        hipIpcCloseMemHandle(peer_mbox_[(size_t)q]);
-        peer_opened_[(size_t)q] = false;
-      }
-    }
-    pbuf_.close_all();
-    try {
-      if (sticky_ == ncclSuccess) boot_.barrier();  // nobody still maps my memory
+      // nobody still writes into my memory: my scratch / mailbox may go to the next
+      // communicator of this process (the peers' imports of them stay open, ipcreg.h)
+      if (sticky_ == ncclSuccess) boot_.barrier();
     } catch (...) {
     }
   }
@@ -374,17 +371,13 @@ Comm::~Comm() {
 }
 
 void Comm::release() {
-  pbuf_.close_all();
-  for (int q = 0; q < (int)peer_opened_.size(); ++q) {
-    if (peer_opened_[(size_t)q]) {
-      hipIpcCloseMemHandle(peer_scratch_[(size_t)q]);
-      hipIpcCloseMemHandle(peer_mbox_[(size_t)q]);
-      peer_opened_[(size_t)q] = false;
-    }
-  }
   boot_.close_all();
-  if (scratch_) hipFree(scratch_);
-  if (mbox_) hipFree(mbox_);
+  // a communicator that failed (sticky error) may still have peers writing into its blocks:
+  // they are not handed to another communicator (the pool keeps them busy)
+  if (sticky_ == ncclSuccess) {
+    ipc::pool_release(scratch_);
+    ipc::pool_release(mbox_);
+  }
   if (pair_seq_) hipFree(pair_seq_);
   if (h_ctl_) hipHostFree(h_ctl_);
   if (stage_) hipFree(stage_);
@@ -485,15 +478,20 @@ ncclResult_t Comm::wait_for(hipStream_t stream, uint32_t seq) {
   return check_status();
 }
 
-// Which memory the kernel can address for a user buffer (see allreduce).
-Comm::Reach Comm::reach(const void* p, const void** kernel_ptr) const {
+// Which memory the kernel can address for a user buffer (see allreduce); *local: plain device
+// memory of this rank's GPU (what the read schedule can share with the peers).
+Comm::Reach Comm::reach(const void* p, const void** kernel_ptr, bool* local) const {
   hipPointerAttribute_t a;
   memset(&a, 0, sizeof a);
+  *local = false;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();
     return Reach::kStaged;  // not known to HIP: pageable host memory
   }
-  if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged) return Reach::kDevice;
+  if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged) {
+    *local = a.type == hipMemoryTypeDevice && !a.isManaged && a.device == device_;
+    return Reach::kDevice;
+  }
   if (a.type == hipMemoryTypeHost && a.devicePointer && !cfg_.stage_host) {
     // device address of p itself (devicePointer / hostPointer may name the allocation base)
     const char* hp = (const char*)(a.hostPointer ? a.hostPointer : p);
@@ -521,16 +519,6 @@ void Comm::ensure_stage(size_t bytes, hipStream_t stream) {
 // Host wait for this communicator's last call (its kernel writes into the peers' memory)
 void Comm::wait_previous_call() {
   if (have_last_) hip_check(hipEventSynchronize(order_ev_), "wait for the previous call");
-}
-
-bool Comm::device_local(const void* p) const {
-  hipPointerAttribute_t a;
-  memset(&a, 0, sizeof a);
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return a.type == hipMemoryTypeDevice && !a.isManaged && a.device == device_;
 }
 
 void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
@@ -624,7 +612,8 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     // through a device staging copy.  Every rank launches the same kernel either way.
     const void* ksend = send;
     void* krecv = recv;
-    const Reach rs = reach(send, &ksend), rr = reach(recv, (const void**)&krecv);
+    bool local_s = false, local_r = false;
+    const Reach rs = reach(send, &ksend, &local_s), rr = reach(recv, (const void**)&krecv, &local_r);
     if (rs == Reach::kStaged || rr == Reach::kStaged) {
       if (cap != hipStreamCaptureStatusNone) {
         fprintf(stderr, "[Mini-NCCL] pageable host buffers cannot be captured into a HIP graph\n");
@@ -655,9 +644,10 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     const char* precv[kMaxRanks] = {};
     int measure = -1;  // calibration: this call's kernel is timed as read (0) / scratch schedule (1)
     if (algo_ == 2 && pbuf_.available()) {
-      // the read schedule: every rank takes part in the rendezvous, all decide alike
-      // a captured call reads through mappings its replays keep using: they are pinned
-      const bool eligible = ksend == send && krecv == recv && device_local(send) && device_local(recv);
+      // the read schedule: every rank takes part in the rendezvous, all decide alike (a captured
+      // call reads through mappings its replays keep using: imports stay open until their owner
+      // frees the allocation, which invalidates the graph anyway)
+      const bool eligible = ksend == send && krecv == recv && local_s && local_r;
       bool vec_all = false;
       PeerBuffers::Decision d = PeerBuffers::kFallback;
       // large auto calls while the measured choice is open (the same predicate on every rank)
@@ -669,7 +659,7 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
         // a peer that does not reach the call within the watchdog's limit fails it, as the
         // kernel's own wait would (the reference's 10 s watchdog, mini_nccl.cu:200-214)
         d = pbuf_.negotiate(send, recv, eligible, count, dtype, op, cfg_.timeout_ms / 1000.0 + 2.0,
-                            [this] { wait_previous_call(); }, psend, precv, &vec_all, capturing, my_t_, max_t);
+                            [this] { wait_previous_call(); }, psend, precv, &vec_all, my_t_, max_t);
       } catch (const PeerGaveUp& e) {
         // a peer's communicator died in an earlier rendezvous: as a peer's ABORT in the kernel
         fprintf(stderr, "[Mini-NCCL] rank %d: %s; communicator is no longer usable\n", rank_, e.what());
@@ -785,22 +775,32 @@ ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gb
   hip_check(hipMalloc((void**)&src, bytes), "probe alloc");
   hip_check(hipMemsetAsync(src, 0x5a, bytes, st), "probe memset");
   std::vector<char*> dst;
-  // user memory: every rank exports a hipMalloc buffer of nranks x bytes; rank d's slice
-  // [rank * bytes, +bytes) is this rank's target there (as the scratch region is)
+  // user memory: every rank exports an ordinary (cached) device buffer of nranks x bytes; rank
+  // d's slice [rank * bytes, +bytes) is this rank's target there (as the scratch region is).
+  // From the process's pool and imported through its registry (ipcreg.h): repeated probes
+  // re-use the buffers and the imports
   char* ub = nullptr;
   std::vector<char*> opened((size_t)nranks_, nullptr);
   if (user) {
-    hip_check(hipMalloc((void**)&ub, bytes * (size_t)nranks_), "probe user buffer");
+    struct UserBuf {
+      hipIpcMemHandle_t h;
+      uint64_t nonce, base, id;
+    } mine;
+    ub = (char*)ipc::pool_acquire(bytes * (size_t)nranks_, 0, &mine.h, &mine.id);
+    mine.nonce = process_nonce();
+    mine.base = (uint64_t)(uintptr_t)ub;
     hip_check(hipMemsetAsync(ub, 0x3c, bytes * (size_t)nranks_, st), "probe memset");
-    hipIpcMemHandle_t mine;
-    hip_check(hipIpcGetMemHandle(&mine, ub), "probe ipc handle");
-    std::vector<hipIpcMemHandle_t> all((size_t)nranks_);
+    std::vector<UserBuf> all((size_t)nranks_);
     boot_.allgather(&mine, all.data(), sizeof mine);
     for (int q = 0; q < nranks_; ++q) {
-      if (q == rank_) continue;
-      void* p = nullptr;
-      hip_check(hipIpcOpenMemHandle(&p, all[(size_t)q], hipIpcMemLazyEnablePeerAccess), "probe ipc open");
-      opened[(size_t)q] = (char*)p;
+      const UserBuf& u = all[(size_t)q];
+      if (q == rank_ || u.nonce == mine.nonce) {
+        opened[(size_t)q] = (char*)(uintptr_t)u.base;
+        continue;
+      }
+      hipError_t e = hipSuccess;
+      opened[(size_t)q] = ipc::open_import(u.nonce, u.base, u.id, u.h, &e);
+      hip_check(opened[(size_t)q] ? hipSuccess : e, "probe ipc open");
     }
   }
   for (int k = 1; k < nranks_; ++k) {
@@ -825,12 +825,7 @@ ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gb
   hip_check(hipEventElapsedTime(&ms, e0, e1), "event time");
   boot_.barrier();  // nobody starts an all-reduce while a peer still writes its slots
   *gbps = (double)bytes * iters / (ms * 1e-3) / 1e9;
-  if (user) {
-    for (char* p : opened)
-      if (p) (void)hipIpcCloseMemHandle(p);
-    boot_.barrier();  // every peer has unmapped my buffer before it is freed
-    hipFree(ub);
-  }
+  if (user) ipc::pool_release(ub);  // every peer is done with it (the barrier above)
   hipEventDestroy(e0);
   hipEventDestroy(e1);
   hipStreamDestroy(st);

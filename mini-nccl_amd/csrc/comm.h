@@ -42,6 +42,7 @@ class Comm {
   double calib_ms(int i) const { return calib_ms_[i & 1]; }
   int last_algo() const { return last_algo_; }  // schedule of the last launched kernel, -1: none
   size_t peer_mappings() const { return pbuf_.mapped_allocations(); }
+  const PeerBuffers& peer_buffers() const { return pbuf_; }
   int scratch_algo() const { return scratch_algo_; }
   // calibration of MINI_NCCL_ALGO=auto with MINI_NCCL_TUNE=1 (max over ranks, ms per call; 0 = not run)
   double tune_ms(int a) const { return tune_ms_[a & 1]; }
@@ -66,12 +67,11 @@ class Comm {
   void tune();
   ncclResult_t wait_for(hipStream_t stream, uint32_t seq);
   enum class Reach { kDevice, kMapped, kStaged };
-  Reach reach(const void* p, const void** kernel_ptr) const;
+  Reach reach(const void* p, const void** kernel_ptr, bool* local) const;
   void ensure_stage(size_t bytes, hipStream_t stream);
   // algo: 0 ring, 1 direct, 2 read (psend / precv: every rank's buffers mapped here)
   void launch(int algo, const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
               uint32_t seq, bool vec, const char* const* psend = nullptr, const char* const* precv = nullptr);
-  bool device_local(const void* p) const;  // device memory of this rank's GPU (not managed)
   void wait_previous_call();
   ncclResult_t check_status();
   // MINI_NCCL_CALIBRATE: read the timings of this rank's measured calls whose events completed
@@ -113,7 +113,8 @@ class Comm {
 
   std::vector<char*> peer_scratch_;
   std::vector<uint64_t*> peer_mbox_;
-  std::vector<bool> peer_opened_;  // true: mapped with hipIpcOpenMemHandle (close on destroy)
+  hipIpcMemHandle_t scratch_h_, mbox_h_;  // exported once (pool blocks, ipcreg.h)
+  uint64_t scratch_id_ = 0, mbox_id_ = 0;
   PeerBuffers pbuf_;               // read schedule: per-call rendezvous + peers' buffer mappings
 
   char* stage_ = nullptr;         // device staging copy for pageable host buffers (grown on demand)

@@ -1,7 +1,9 @@
 // peerbuf.cpp -- see peerbuf.h.
 #include "peerbuf.h"
 
+#include <errno.h>
 #include <fcntl.h>
+#include <pthread.h>
 #include <sched.h>
 #include <sys/mman.h>
 #include <time.h>
@@ -12,15 +14,18 @@
 #include <cstring>
 #include <stdexcept>
 
+#include "ipcreg.h"
 #include "kernels.h"
 
 namespace mnccl {
 
 namespace {
 
-constexpr uint32_t kBoardMagic = 0x4d4e4252u;  // 'MNBR'
+constexpr uint32_t kBoardMagic = 0x4d4e4253u;  // 'MNBS'
 constexpr int kBoardDepth = 16;                // records per rank in flight (calls ahead of the slowest peer)
-constexpr size_t kMaxExports = 64, kMaxMappings = 64;
+constexpr int kMaxFreed = 8;                   // freed allocations one record reports (the rest: next calls)
+constexpr size_t kMaxImports = 1024;           // peer allocations mapped per process; beyond: scratch schedule
+constexpr size_t kMaxKnown = 4096;
 
 double now_s() {
   struct timespec ts;
@@ -47,6 +52,8 @@ struct alignas(64) CallRec {
   int32_t dtype, op, eligible, aligned;
   BufDesc send, recv;
   float t[2];  // this rank's calibration timings so far (Comm: read, scratch schedule; 0 = unknown)
+  int32_t nfreed;
+  uint64_t freed[kMaxFreed][2];  // (base, id) of this rank's exported allocations freed since its last record
   // second round (only when some rank may have to open a new mapping): the call whose mapping
   // outcome map_ok reports, stored after it (release)
   alignas(64) std::atomic<uint64_t> mapped;
@@ -59,6 +66,9 @@ struct alignas(64) Counter {
 
 struct Board {
   uint32_t magic, nranks;
+  // serialises hipIpcOpenMemHandle / hipIpcCloseMemHandle across the ranks' processes (robust:
+  // a process that dies holding it does not block the others)
+  alignas(64) pthread_mutex_t ipc_lock;
   Counter consumed[kMaxRanks];  // last call whose records rank q has read
   Counter gave_up[kMaxRanks];   // != 0: rank q abandoned a rendezvous (its communicator is dead)
   CallRec rec[kMaxRanks][kBoardDepth];
@@ -67,7 +77,7 @@ struct Board {
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "the board needs address-free atomics");
 
 PeerBuffers::~PeerBuffers() {
-  close_all();
+  // imports stay open (ipcreg.h): a later communicator of this process reuses them
   if (board_) munmap(board_, board_bytes_);
   board_ = nullptr;
 }
@@ -76,6 +86,10 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
   rank_ = rank;
   nranks_ = nranks;
   nonces_ = nonces;
+  if (!test_fake_ && hipGetDevice(&device_) != hipSuccess) {
+    (void)hipGetLastError();
+    device_ = -1;
+  }
   board_bytes_ = (sizeof(Board) + 4095) & ~(size_t)4095;
   // rank 0 creates the segment under a name unique to this communicator and shares it; every
   // rank maps it; once all have, rank 0 unlinks it (nothing is left in /dev/shm, even if a
@@ -102,8 +116,17 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
     close(fd);
   }
   int ok = m != MAP_FAILED ? 1 : 0;
+  if (ok && rank == 0) {
+    Board* b = static_cast<Board*>(m);
+    pthread_mutexattr_t a;
+    ok = pthread_mutexattr_init(&a) == 0 && pthread_mutexattr_setpshared(&a, PTHREAD_PROCESS_SHARED) == 0 &&
+         pthread_mutexattr_setrobust(&a, PTHREAD_MUTEX_ROBUST) == 0 && pthread_mutex_init(&b->ipc_lock, &a) == 0;
+    pthread_mutexattr_destroy(&a);
+    b->magic = kBoardMagic;
+    b->nranks = (uint32_t)nranks;
+  }
   std::vector<int> oks((size_t)nranks);
-  boot.allgather(&ok, oks.data(), sizeof ok);
+  boot.allgather(&ok, oks.data(), sizeof ok);  // also: rank 0's board is initialised
   if (rank == 0 && names[0]) shm_unlink(names.data());
   bool all = true;
   for (int v : oks) all = all && v;
@@ -112,13 +135,20 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
     return;  // no board anywhere: the read schedule falls back on every rank
   }
   board_ = static_cast<Board*>(m);
-  if (rank == 0) {
-    board_->magic = kBoardMagic;
-    board_->nranks = (uint32_t)nranks;
-  }
-  boot.barrier();  // the zeroed board is initialised before anyone negotiates
+  boot.barrier();  // the board is initialised before anyone negotiates
 }
 
+void PeerBuffers::lock() {
+  const int e = pthread_mutex_lock(&board_->ipc_lock);
+  if (e == EOWNERDEAD) pthread_mutex_consistent(&board_->ipc_lock);  // its holder died: nothing to repair
+}
+
+void PeerBuffers::unlock() { pthread_mutex_unlock(&board_->ipc_lock); }
+
+size_t PeerBuffers::mapped_allocations() const { return test_fake_ ? fake_maps_.size() : ipc::imports(); }
+
+// (base, id, handle) of the allocation holding p, exported once; false: it cannot be shared
+// (not a plain device allocation, or its address was exported before for another allocation)
 bool PeerBuffers::describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMemHandle_t* h) {
   if (test_fake_) {  // CPU self-test: the pointer's page is its "allocation", the value its id
     *base = (uint64_t)(uintptr_t)p & ~(uint64_t)4095;
@@ -127,93 +157,52 @@ bool PeerBuffers::describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMe
     return true;
   }
   hipDeviceptr_t b = 0;
-  size_t sz = 0;
   unsigned long long bid = 0;
-  if (hipMemGetAddressRange(&b, &sz, (hipDeviceptr_t)p) != hipSuccess ||
-      hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+  hipPointer_attribute attrs[2] = {HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, HIP_POINTER_ATTRIBUTE_BUFFER_ID};
+  void* vals[2] = {&b, &bid};
+  if (hipDrvPointerGetAttributes(2, attrs, vals, (hipDeviceptr_t)p) != hipSuccess || !b) {
     (void)hipGetLastError();
     return false;
   }
   *base = (uint64_t)(uintptr_t)b;
   *id = bid;
-  for (const Export& e : exports_)
-    if (e.base == *base && e.id == bid) {
-      *h = e.h;
-      return true;
-    }
-  if (hipIpcGetMemHandle(h, (void*)b) != hipSuccess) {  // e.g. a virtual-memory-managed allocation
-    (void)hipGetLastError();
-    return false;
-  }
-  if (exports_.size() >= kMaxExports) exports_.erase(exports_.begin());
-  exports_.push_back(Export{*base, bid, *h});
-  return true;
+  return ipc::export_allocation(*base, bid, h);
 }
 
-char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h,
-                            const std::function<void()>& sync_previous, bool pin) {
-  for (Mapping& m : peers_)
-    if (m.rank == q && m.base == base && m.id == id) {
-      m.last_use = seq_;
-      m.pinned = m.pinned || pin;
-      return m.local;
-    }
+// rank q's allocation (base, id) mapped here; nullptr (and *why) if it cannot be.  Caller holds
+// the board lock.
+char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h, std::string* why) {
   if (test_fake_) {  // CPU self-test: no HIP; fail on the chosen call
-    if (seq_ == test_fail_call_) throw std::runtime_error("read schedule: injected mapping failure (self-test)");
-    peers_.push_back(Mapping{q, base, id, (char*)(uintptr_t)base, seq_, pin});
-    if (peers_.size() > kMaxMappings) peers_.erase(peers_.begin());
+    for (const Known& k : fake_maps_)
+      if (k.rank == q && k.base == base && k.id == id) return (char*)(uintptr_t)base;
+    if (seq_ == test_fail_call_) {
+      *why = "injected mapping failure (self-test)";
+      return nullptr;
+    }
+    fake_maps_.push_back(Known{q, base, id});
     return (char*)(uintptr_t)base;
   }
-  void* p = nullptr;
-  hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-  // an open can fail transiently; retry a few times before failing the call (every failure
-  // and retry is reported)
-  for (int attempt = 1; e != hipSuccess && attempt <= 5; ++attempt) {
-    (void)hipGetLastError();
-    char hx[129];
-    for (int i = 0; i < 64; ++i) snprintf(hx + 2 * i, 3, "%02x", (unsigned char)h.reserved[i]);
-    fprintf(stderr,
-            "[Mini-NCCL] rank %d: hipIpcOpenMemHandle of rank %d's allocation (base 0x%llx, id %llu) failed: %s; "
-            "%zu mappings open, handle %s; retry %d\n",
-            rank_, q, (unsigned long long)base, (unsigned long long)id, hipGetErrorString(e), peers_.size(), hx, attempt);
-    usleep(1000u << attempt);
-    e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  const uint64_t owner = nonces_[(size_t)q];
+  if (char* p = ipc::find_import(owner, base, id)) return p;
+  if (ipc::imports() >= kMaxImports) {
+    *why = "the process maps " + std::to_string(kMaxImports) + " peer allocations already";
+    return nullptr;
   }
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    throw std::runtime_error(std::string("read schedule: hipIpcOpenMemHandle of rank ") + std::to_string(q) +
-                             "'s buffer: " + hipGetErrorString(e));
+  hipError_t e = hipSuccess;
+  char* p = ipc::open_import(owner, base, id, h, &e);
+  if (!p) {
+    char msg[256];
+    snprintf(msg, sizeof msg, "hipIpcOpenMemHandle of rank %d's allocation (base 0x%llx, id %llu): %s", q,
+             (unsigned long long)base, (unsigned long long)id, hipGetErrorString(e));
+    *why = msg;
   }
-  peers_.push_back(Mapping{q, base, id, (char*)p, seq_, pin});
-  // over the bound: the least recently used (unpinned) mapping goes, AFTER the new one is open
-  // (a close immediately followed by an open could hand the new import the address range the
-  // runtime is still releasing); the last kernel may still read through it, so wait for it
-  size_t unpinned = 0;
-  for (const Mapping& m : peers_) unpinned += m.pinned ? 0 : 1;
-  if (unpinned > kMaxMappings) {
-    size_t lru = peers_.size();
-    for (size_t i = 0; i < peers_.size(); ++i)
-      if (!peers_[i].pinned && (lru == peers_.size() || peers_[i].last_use < peers_[lru].last_use)) lru = i;
-    sync_previous();
-    (void)hipIpcCloseMemHandle(peers_[lru].local);
-    (void)hipGetLastError();
-    peers_.erase(peers_.begin() + (long)lru);
-  }
-  return (char*)p;
-}
-
-void PeerBuffers::close_all() {
-  if (!test_fake_)
-    for (Mapping& m : peers_) (void)hipIpcCloseMemHandle(m.local);
-  peers_.clear();
-  (void)hipGetLastError();
+  return p;
 }
 
 PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv, bool eligible, uint64_t count,
                                              int dtype, int op, double timeout_s,
                                              const std::function<void()>& sync_previous, const char** psend,
-                                             const char** precv, bool* vec_all, bool pin, const float* my_t,
-                                             float* max_t) {
+                                             const char** precv, bool* vec_all, const float* my_t, float* max_t) {
   const uint64_t k = ++seq_;
   const double t0 = now_s();
   auto wait = [&](const std::atomic<uint64_t>& v, uint64_t want, int q, const char* what) {
@@ -228,12 +217,12 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
     }
   };
   try {
-    return negotiate_body(k, send, recv, eligible, count, dtype, op, sync_previous, psend, precv, vec_all, pin,
-                          my_t, max_t, wait);
+    return negotiate_body(k, send, recv, eligible, count, dtype, op, sync_previous, psend, precv, vec_all, my_t, max_t,
+                          wait);
   } catch (...) {
-    // this rank gives up (a peer that never came or gave up itself, a mapping that failed): say
-    // so on the board, so every peer waiting in a rendezvous with it fails at once instead of at
-    // its own limit (the abandonment cascades through the ranks)
+    // this rank gives up (a peer that never came or gave up itself): say so on the board, so
+    // every peer waiting in a rendezvous with it fails at once instead of at its own limit (the
+    // abandonment cascades through the ranks)
     board_->gave_up[rank_].v.store(k, std::memory_order_release);
     throw;
   }
@@ -243,13 +232,17 @@ template <typename Wait>
 PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible,
                                                   uint64_t count, int dtype, int op,
                                                   const std::function<void()>& sync_previous, const char** psend,
-                                                  const char** precv, bool* vec_all, bool pin, const float* my_t,
-                                                  float* max_t, const Wait& wait) {
+                                                  const char** precv, bool* vec_all, const float* my_t, float* max_t,
+                                                  const Wait& wait) {
   const int slot = (int)(k % kBoardDepth);
   // my record slot is free once every peer has read the record kBoardDepth calls back
   if (k > (uint64_t)kBoardDepth)
     for (int q = 0; q < nranks_; ++q)
       if (q != rank_) wait(board_->consumed[q].v, k - kBoardDepth, q, "finish reading the records before");
+
+  // allocations I exported and have freed since my last call: my peers close their imports
+  if (!test_fake_)
+    for (const auto& f : ipc::reap_freed_exports()) freed_.push_back(f);
 
   CallRec& me = board_->rec[rank_][slot];
   BufDesc sd, rd;
@@ -269,12 +262,21 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
   me.recv = rd;
   me.t[0] = my_t ? my_t[0] : 0.f;
   me.t[1] = my_t ? my_t[1] : 0.f;
+  me.nfreed = 0;
+  while (!freed_.empty() && me.nfreed < kMaxFreed) {
+    me.freed[me.nfreed][0] = freed_.front().first;
+    me.freed[me.nfreed][1] = freed_.front().second;
+    ++me.nfreed;
+    freed_.pop_front();
+  }
   me.seq.store(k, std::memory_order_release);
 
   struct Seen {
     uint64_t count;
     int32_t dtype, op, eligible, aligned;
     BufDesc send, recv;
+    int32_t nfreed;
+    uint64_t freed[kMaxFreed][2];
   };
   std::vector<Seen> recs((size_t)nranks_);
   float tmax[2] = {0.f, 0.f};
@@ -282,14 +284,53 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
   for (int q = 0; q < nranks_; ++q) {
     const CallRec& c = board_->rec[q][slot];
     if (q != rank_) wait(c.seq, k, q, "reach");
-    recs[(size_t)q] = Seen{c.count, c.dtype, c.op, c.eligible, c.aligned, c.send, c.recv};
+    Seen& s = recs[(size_t)q];
+    s.count = c.count;
+    s.dtype = c.dtype;
+    s.op = c.op;
+    s.eligible = c.eligible;
+    s.aligned = c.aligned;
+    s.send = c.send;
+    s.recv = c.recv;
+    s.nfreed = c.nfreed < 0 ? 0 : c.nfreed > kMaxFreed ? kMaxFreed : c.nfreed;
+    memcpy(s.freed, c.freed, sizeof s.freed);
     for (int i = 0; i < 2; ++i) {
       tall[i] = tall[i] && c.t[i] > 0.f;
       tmax[i] = c.t[i] > tmax[i] ? c.t[i] : tmax[i];
     }
   }
+  board_->consumed[rank_].v.store(k, std::memory_order_release);  // my copies are taken
   if (max_t)  // every rank's timing known -> their max (what every rank reads alike), else 0
     for (int i = 0; i < 2; ++i) max_t[i] = tall[i] ? tmax[i] : 0.f;
+
+  // the peers' freed allocations: forget them (every rank alike) and close my imports of them.
+  // The owner's call that used one last ended only after every peer's kernel was done with it
+  // (read_kernel's DONE); my own last kernel is waited for all the same.
+  bool synced = false;
+  for (int q = 0; q < nranks_; ++q)
+    for (int i = 0; i < recs[(size_t)q].nfreed; ++i) {
+      const uint64_t fb = recs[(size_t)q].freed[i][0], fi = recs[(size_t)q].freed[i][1];
+      known_.erase(Known{q, fb, fi});
+      if (q == rank_ || nonces_[(size_t)q] == nonces_[(size_t)rank_]) continue;
+      if (test_fake_) {
+        for (size_t j = 0; j < fake_maps_.size(); ++j)
+          if (fake_maps_[j] == Known{q, fb, fi}) {
+            fake_maps_.erase(fake_maps_.begin() + (long)j);
+            ++closed_freed_;
+            break;
+          }
+        continue;
+      }
+      if (!ipc::find_import(nonces_[(size_t)q], fb, fi)) continue;
+      if (!synced) {
+        sync_previous();
+        synced = true;
+      }
+      lock();
+      closed_freed_ += ipc::close_import(nonces_[(size_t)q], fb, fi) ? 1 : 0;
+      unlock();
+    }
+
   bool all = true, mismatch = false, aligned = true;
   for (const Seen& c : recs) {
     all = all && c.eligible;
@@ -297,52 +338,52 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
     mismatch = mismatch || c.count != count || c.dtype != dtype || c.op != op;
   }
   const Decision d = mismatch ? kMismatch : all ? kRead : kFallback;
-  if (d != kRead) {
-    board_->consumed[rank_].v.store(k, std::memory_order_release);  // my copies are taken
-    return d;
-  }
-  // Would any rank have to open a mapping?  Every buffer used by a read call in the last
-  // `horizon` read calls is still mapped by every other rank (each keeps its kMaxMappings most
-  // recently used; those calls used at most 2(n-1) per rank), so if every buffer of this call is
-  // among them, no rank opens anything -- the common case of a caller reusing its buffers -- and
-  // no second round is needed.  Computed from the records alone: every rank reaches the same
-  // answer.
-  const size_t horizon = kMaxMappings / (size_t)(2 * (nranks_ > 1 ? nranks_ - 1 : 1));
-  auto recent = [&](int q, const BufDesc& b) {
-    for (const auto& call : recent_)
-      for (const RecentKey& x : call)
-        if (x.rank == q && x.base == b.base && x.id == b.id) return true;
-    return false;
-  };
+  *vec_all = aligned;
+  if (d != kRead) return d;
+  // Would any rank have to open a mapping?  A buffer some earlier read call ran on, and whose
+  // owner has not reported it freed since, is still mapped by every rank (imports stay open), so
+  // if every buffer of this call is one -- the common case of a caller reusing its buffers -- no
+  // rank opens anything and no second round is needed.  Decided from the records alone: every
+  // rank reaches the same answer.
   bool need_agree = false;
   for (int q = 0; q < nranks_ && !need_agree; ++q)
-    need_agree = !recent(q, recs[(size_t)q].send) || !recent(q, recs[(size_t)q].recv);
+    need_agree = !known_.count(Known{q, recs[(size_t)q].send.base, recs[(size_t)q].send.id}) ||
+                 !known_.count(Known{q, recs[(size_t)q].recv.base, recs[(size_t)q].recv.id});
   bool mapped = true;
   std::string why;
-  for (int q = 0; q < nranks_; ++q) {
+  bool locked = false;
+  for (int q = 0; q < nranks_ && mapped; ++q) {
     const Seen& c = recs[(size_t)q];
     if (q == rank_ || nonces_[(size_t)q] == nonces_[(size_t)rank_]) {
       psend[q] = (const char*)(uintptr_t)c.send.raw;  // this process's address space
       precv[q] = (const char*)(uintptr_t)c.recv.raw;
       continue;
     }
-    if (!mapped) continue;
-    try {
-      psend[q] = map_peer(q, c.send.base, c.send.id, c.send.h, sync_previous, pin) + c.send.off;
-      precv[q] = map_peer(q, c.recv.base, c.recv.id, c.recv.h, sync_previous, pin) + c.recv.off;
-    } catch (const std::runtime_error& e) {
-      if (!need_agree) throw;  // cannot happen (nothing new to open); fail loudly if it does
-      mapped = false;
-      why = e.what();
+    if (!locked && need_agree) {  // opens may happen: serialised with every process's opens / closes
+      lock();
+      locked = true;
     }
+    const char* s = map_peer(q, c.send.base, c.send.id, c.send.h, &why);
+    const char* r = s ? map_peer(q, c.recv.base, c.recv.id, c.recv.h, &why) : nullptr;
+    if (!s || !r) {
+      mapped = false;
+      ++map_failures_;
+      break;
+    }
+    psend[q] = s + c.send.off;
+    precv[q] = r + c.recv.off;
   }
+  if (locked) unlock();
+  if (!mapped && !need_agree)  // cannot happen (every buffer is mapped already); fail loudly if it does
+    throw std::runtime_error("read schedule: a mapping of a known buffer is missing: " + why);
   Decision out = kRead;
   if (need_agree) {
     // second round: every rank's mapping outcome; one failure -> the scratch schedule for this
     // call on every rank (same bits, no buffer of a peer is read)
     ++agreements_;
-    me.map_ok = mapped ? 1 : 0;
-    me.mapped.store(k, std::memory_order_release);
+    CallRec& mine = board_->rec[rank_][slot];
+    mine.map_ok = mapped ? 1 : 0;
+    mine.mapped.store(k, std::memory_order_release);
     int failed = -1;
     for (int q = 0; q < nranks_; ++q) {
       const CallRec& c = board_->rec[q][slot];
@@ -355,17 +396,15 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
       out = kFallback;
     }
   }
-  board_->consumed[rank_].v.store(k, std::memory_order_release);  // my copies are taken
   if (out == kRead) {
-    std::vector<RecentKey> keys;
-    for (int q = 0; q < nranks_; ++q) {
-      keys.push_back(RecentKey{q, recs[(size_t)q].send.base, recs[(size_t)q].send.id});
-      keys.push_back(RecentKey{q, recs[(size_t)q].recv.base, recs[(size_t)q].recv.id});
+    for (int q = 0; q < nranks_; ++q)
+      for (const BufDesc* b : {&recs[(size_t)q].send, &recs[(size_t)q].recv})
+        if (known_.insert(Known{q, b->base, b->id}).second) known_order_.push_back(Known{q, b->base, b->id});
+    while (known_order_.size() > kMaxKnown) {  // forgetting only brings back a mapping round
+      known_.erase(known_order_.front());
+      known_order_.pop_front();
     }
-    recent_.push_back(std::move(keys));
-    while (recent_.size() > horizon) recent_.pop_front();
   }
-  *vec_all = aligned;
   return out;
 }
 

@@ -5,13 +5,14 @@
 // address space.  The reference exchanged IPC handles of the user buffers through rank 0 on
 // EVERY call over TCP and opened/closed them each time (RDMATransport.h:171-257).  Here:
 //  * each rank publishes a small record per call -- (allocation base, allocation id, offset, HIP
-//    IPC handle) of send and recv, count / dtype / op, and whether it can take part -- on a
-//    board in host shared memory (one node: every rank is on this host), read by its peers
-//    with no network round trip;
-//  * a peer's allocation is opened once (hipIpcOpenMemHandle) and cached by (rank, base, id):
-//    the id (HIP_POINTER_ATTRIBUTE_BUFFER_ID) is new for every allocation, so a freed and
-//    re-allocated address is never served from a stale mapping ("key the IPC
-//    cache by (base pointer, size) and tolerate address reuse");
+//    IPC handle) of send and recv, count / dtype / op, whether it can take part, and which of
+//    its earlier exported allocations it has freed since -- on a board in host shared memory
+//    (one node: every rank is on this host), read by its peers with no network round trip;
+//  * a peer's allocation is opened once and kept open until its owner reports it freed (ipcreg.h:
+//    ROCm's IPC can map the wrong memory when an allocation is re-opened after a close, or a
+//    re-used address is exported again, so neither ever happens); opens and closes of all the
+//    communicator's processes are serialised by a lock on the board (an open racing another
+//    process's close can fail);
 //  * every rank reads the same records, so every rank takes the same decision: the read
 //    schedule when all ranks can, the communicator's scratch schedule otherwise, an error when
 //    the ranks disagree on count / dtype / op.
@@ -23,6 +24,7 @@
 #include <functional>
 #include <stdexcept>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "bootstrap.h"
@@ -50,24 +52,23 @@ class PeerBuffers {
   bool available() const { return board_ != nullptr; }
 
   enum Decision { kRead = 1, kFallback = 0, kMismatch = -1 };
-  // One call's rendezvous.  `eligible`: this rank's buffers are device memory of this GPU.  On kRead, psend / precv[q] hold rank q's buffers mapped
-  // here (this rank's own at [rank]) and *vec_all whether every rank's buffers are dword-aligned.
-  // `sync_previous` waits for this communicator's last kernel (before a cached mapping is
-  // closed).  Throws std::runtime_error when a peer does not arrive within timeout_s.
-  // `pin`: the call is being captured into a graph whose replays will read through these
-  // mappings: they are never evicted (closed only with the communicator).
+  // One call's rendezvous.  `eligible`: this rank's buffers are device memory (the rendezvous
+  // also requires them to be memory of this rank's GPU, and shareable).  On kRead, psend /
+  // precv[q] hold rank q's buffers mapped here (this rank's own at [rank]) and *vec_all whether
+  // every rank's buffers are dword-aligned.  `sync_previous` waits for this communicator's last
+  // kernel (before a freed peer allocation's mapping is closed).  Throws std::runtime_error when
+  // a peer does not arrive within timeout_s.
   // my_t / max_t (optional): two timings this rank publishes with its record, and per timing
   // the max over every rank's published value, or 0 while some rank's is still unknown (0).
   Decision negotiate(const void* send, const void* recv, bool eligible, uint64_t count, int dtype, int op,
                      double timeout_s, const std::function<void()>& sync_previous, const char** psend,
-                     const char** precv, bool* vec_all, bool pin = false, const float* my_t = nullptr,
-                     float* max_t = nullptr);
-  // Unmaps every peer allocation; call when no kernel of this communicator can still run.
-  void close_all();
+                     const char** precv, bool* vec_all, const float* my_t = nullptr, float* max_t = nullptr);
 
   // for tests / diagnostics
-  size_t mapped_allocations() const { return peers_.size(); }
+  size_t mapped_allocations() const;                    // peer allocations mapped in this process
   uint64_t agreements() const { return agreements_; }  // calls that needed the mapping round
+  uint64_t map_failures() const { return map_failures_; }  // opens that failed (any rank's call fell back)
+  uint64_t closed_freed() const { return closed_freed_; }  // imports closed because their owner freed them
   // CPU self-test only (no GPU): describe() returns synthetic (base, id) from the pointer value,
   // map_peer() returns the owner's raw address, and map_peer() fails on call `fail_call` (0:
   // never), as a failed hipIpcOpenMemHandle would
@@ -75,40 +76,42 @@ class PeerBuffers {
     test_fake_ = fake;
     test_fail_call_ = fail_call;
   }
+  // CPU self-test: report this rank's allocation (base, id) freed with its next record
+  void test_report_freed(uint64_t base, uint64_t id) { freed_.emplace_back(base, id); }
 
  private:
-  struct Export {
-    uint64_t base, id;
-    hipIpcMemHandle_t h;
-  };
-  struct Mapping {
-    int rank;
-    uint64_t base, id;  // in the owner's process
-    char* local;        // the allocation base mapped here
-    uint64_t last_use;
-    bool pinned;        // used by a captured graph: never evicted
-  };
   template <typename Wait>
   Decision negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible, uint64_t count, int dtype,
                           int op, const std::function<void()>& sync_previous, const char** psend, const char** precv,
-                          bool* vec_all, bool pin, const float* my_t, float* max_t, const Wait& wait);
+                          bool* vec_all, const float* my_t, float* max_t, const Wait& wait);
   bool describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMemHandle_t* h);
-  char* map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h,
-                 const std::function<void()>& sync_previous, bool pin);
+  char* map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h, std::string* why);
+  void lock();
+  void unlock();
 
   Board* board_ = nullptr;
   size_t board_bytes_ = 0;
   int rank_ = 0, nranks_ = 0;
+  int device_ = -1;
   std::vector<uint64_t> nonces_;
   uint64_t seq_ = 0;  // calls negotiated so far
-  std::vector<Export> exports_;
-  std::vector<Mapping> peers_;
-  struct RecentKey {
+  // allocations this rank exported and has since freed, not yet published
+  std::deque<std::pair<uint64_t, uint64_t>> freed_;
+  // (rank, base, id) of every buffer a read call ran on and no owner has reported freed since:
+  // every rank still maps them (imports stay open until then), so a call whose buffers are all
+  // here needs no mapping round.  Derived from the records alone: the same on every rank.
+  struct Known {
     int rank;
     uint64_t base, id;
+    bool operator==(const Known& o) const { return rank == o.rank && base == o.base && id == o.id; }
   };
-  std::deque<std::vector<RecentKey>> recent_;  // buffers of the last read calls (every rank alike)
-  uint64_t agreements_ = 0;
+  struct KnownHash {
+    size_t operator()(const Known& k) const { return std::hash<uint64_t>{}(k.base ^ (k.id << 20) ^ (uint64_t)k.rank); }
+  };
+  std::unordered_set<Known, KnownHash> known_;
+  std::deque<Known> known_order_;  // insertion order, to bound known_
+  std::vector<Known> fake_maps_;   // CPU self-test: the "imports"
+  uint64_t agreements_ = 0, map_failures_ = 0, closed_freed_ = 0;
   bool test_fake_ = false;
   uint64_t test_fail_call_ = 0;
 };

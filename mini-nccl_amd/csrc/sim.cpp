@@ -436,8 +436,10 @@ int mnccl_board_selftest(int rank, int nranks, const char* ip, int port, int sce
     // scenarios 4 / 5: every rank eligible with synthetic buffers (no HIP); 4: rank 1 cannot map
     // on call 3 (every rank must fall back on that call alone); 5: the same buffers every call
     // after the first (the mapping round runs once), except a fresh buffer on call calls/2
+    // scenario 6: as 5, and at call calls/2 every rank reports its first buffers freed (its
+    // peers close their mappings of them, every rank forgets them)
     std::vector<char> arena(1 << 20);
-    const bool fake = scenario == 4 || scenario == 5;
+    const bool fake = scenario == 4 || scenario == 5 || scenario == 6;
     if (fake) pb.set_test_fake(true, scenario == 4 && rank == 1 ? 3u : 0u);
     uint64_t rng = 0x9E3779B97F4A7C15ull * (uint64_t)(rank + 1);
     for (int i = 0; i < calls; ++i) decisions[i] = 99;
@@ -457,13 +459,19 @@ int mnccl_board_selftest(int rank, int nranks, const char* ip, int port, int sce
         if (scenario == 4) {  // a new send / recv page every call
           sb = arena.data() + (size_t)(2 * i) * 4096 % arena.size();
           rb = arena.data() + (size_t)(2 * i + 1) * 4096 % arena.size();
-        } else if (scenario == 5) {
-          const int gen = i == calls / 2 ? 1 : 0;
+        } else if (scenario == 5 || scenario == 6) {
+          const int gen = scenario == 6 ? (i >= calls / 2 ? 1 : 0) : i == calls / 2 ? 1 : 0;
+          if (scenario == 6 && i == calls / 2)
+            for (int g = 0; g < 2; ++g) {
+              const char* p = arena.data() + (size_t)g * 4096;
+              pb.test_report_freed((uint64_t)(uintptr_t)p & ~(uint64_t)4095, (uint64_t)(uintptr_t)p);
+            }
           sb = arena.data() + (size_t)(2 * gen) * 4096;
           rb = arena.data() + (size_t)(2 * gen + 1) * 4096;
         }
         decisions[i] = (int)pb.negotiate(sb, rb, fake, count, 7, 0, timeout_s, [] {}, ps, pr, &vec);
         if (fake) decisions[i] += 10 * (int)pb.agreements();  // decision + 10 x mapping rounds so far
+        if (scenario == 6) decisions[i] += 1000 * (int)pb.closed_freed();  // + 1000 x mappings closed
       } catch (const std::runtime_error&) {
         decisions[i] = -9;
         break;

@@ -51,6 +51,9 @@ class CommInfo(ctypes.Structure):
         ("pipelines", ctypes.c_int), ("ranks_on_device", ctypes.c_int), ("slot_bytes", ctypes.c_size_t),
         ("last_algo", ctypes.c_int), ("peer_mappings", ctypes.c_size_t), ("scratch_algo", ctypes.c_int),
         ("calib_choice", ctypes.c_int), ("calib_ms", ctypes.c_double * 2),
+        # since mncclVersion 300
+        ("ipc_open_failures", ctypes.c_ulonglong), ("read_map_failures", ctypes.c_ulonglong),
+        ("read_rounds", ctypes.c_ulonglong), ("closed_freed", ctypes.c_ulonglong), ("live_exports", ctypes.c_size_t),
     ]
 
 
@@ -66,6 +69,7 @@ SIGNATURES = {
     "mncclLocalReduce": (_I, [_VP, _VP, _VP, _SZ, _I, _I, _VP]),
     "mncclCommGetAsyncError": (_I, [_VP, ctypes.POINTER(_I)]),
     "mncclCommGetInfo": (_I, [_VP, ctypes.POINTER(CommInfo)]),
+    "mncclCommGetInfoV": (_I, [_VP, _VP, _SZ]),
     "mncclCommSetAlgo": (_I, [_VP, _I]),
     "mncclCommLinkProbe": (_I, [_VP, _I, _SZ, _I, ctypes.POINTER(ctypes.c_double)]),
     "mncclVersion": (_I, []),
@@ -131,7 +135,7 @@ class Comm:
 
     def info(self):
         i = CommInfo()
-        check(load().mncclCommGetInfo(self.handle, ctypes.byref(i)))
+        check(load().mncclCommGetInfoV(self.handle, ctypes.byref(i), ctypes.sizeof(i)))
         d = {f: getattr(i, f) for f, _ in CommInfo._fields_}
         d["tune_ms"] = list(d["tune_ms"])
         d["calib_ms"] = list(d["calib_ms"])

@@ -78,8 +78,10 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
             def placement(key, dflt):
                 m = case.get(key, dflt)
                 return m[rank % len(m)] if isinstance(m, (list, tuple)) else m
-            send = hip_rt.buffer(placement("mem", "device"), nbytes + off)
-            recv = send if inplace else hip_rt.buffer(placement("recv_mem", placement("mem", "device")), nbytes + off)
+            fresh = case.get("fresh", False)  # own hipMalloc / hipFree (allocation churn), not the cache
+            send = hip_rt.buffer(placement("mem", "device"), nbytes + off, fresh)
+            recv = send if inplace else hip_rt.buffer(placement("recv_mem", placement("mem", "device")), nbytes + off,
+                                                      fresh)
             if not inplace:
                 recv.fill_byte(0xAB)
             rc = 0
@@ -120,7 +122,9 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
             ci = comm.info()
             results.append({"case": case, "rc": rc, "bad": bad, "first": first, "detail": detail, "secs": dt,
                             "async": comm.async_error(), "last_algo": ci["last_algo"],
-                            "peer_mappings": ci["peer_mappings"]})
+                            "peer_mappings": ci["peer_mappings"], "ipc_open_failures": ci["ipc_open_failures"],
+                            "read_map_failures": ci["read_map_failures"], "closed_freed": ci["closed_freed"],
+                            "live_exports": ci["live_exports"]})
             send.free()
             if not inplace:
                 recv.free()

@@ -68,11 +68,34 @@ def set_device(d):
     check(lib().hipSetDevice(d), "hipSetDevice")
 
 
+_cache = {}  # segment bytes -> free segments (device pointers) of that size
+
+
+def _segment_bytes(nbytes):
+    """A caching allocator's segment size, as frameworks use (torch's caching allocator never
+    hipFrees a segment it can hand out again): a power of two of at least 2 MiB."""
+    s = 2 << 20
+    while s < nbytes:
+        s <<= 1
+    return s
+
+
 class DeviceBuffer:
-    def __init__(self, nbytes):
+    """Device memory.  By default from a per-process cache of whole segments (a freed buffer's
+    segment serves the next request of the same segment size: the allocation -- and so its IPC
+    export -- is reused, as with torch's caching allocator); fresh=True: its own hipMalloc /
+    hipFree, for the tests of allocation churn."""
+
+    def __init__(self, nbytes, fresh=False):
         self.nbytes = nbytes
+        self.fresh = fresh
+        self.seg = max(nbytes, 16) if fresh else _segment_bytes(nbytes)
+        free = [] if fresh else _cache.get(self.seg, [])
+        if free:
+            self.ptr = free.pop()
+            return
         p = ctypes.c_void_p()
-        check(lib().hipMalloc(ctypes.byref(p), max(nbytes, 16)), "hipMalloc")
+        check(lib().hipMalloc(ctypes.byref(p), self.seg), "hipMalloc")
         self.ptr = p.value
 
     def upload(self, arr, offset=0):
@@ -92,7 +115,10 @@ class DeviceBuffer:
 
     def free(self):
         if self.ptr:
-            lib().hipFree(self.ptr)
+            if self.fresh:
+                lib().hipFree(self.ptr)
+            else:
+                _cache.setdefault(self.seg, []).append(self.ptr)
             self.ptr = 0
 
 
@@ -139,8 +165,10 @@ class PageableBuffer(HostBuffer):
         self.ptr = 0
 
 
-def buffer(kind, nbytes):
-    return {"device": DeviceBuffer, "pinned": HostBuffer, "pageable": PageableBuffer}[kind](nbytes)
+def buffer(kind, nbytes, fresh=False):
+    if kind == "device":
+        return DeviceBuffer(nbytes, fresh=fresh)
+    return {"pinned": HostBuffer, "pageable": PageableBuffer}[kind](nbytes)
 
 
 class Stream:

@@ -103,14 +103,16 @@ def test_read_schedule_rendezvous_across_processes(sim_lib, world, scenario):
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
-@pytest.mark.parametrize("scenario", [4, 5], ids=["map-failure", "reused-buffers"])
+@pytest.mark.parametrize("scenario", [4, 5, 6], ids=["map-failure", "reused-buffers", "freed-buffers"])
 def test_read_schedule_mapping_round(sim_lib, world, scenario):
     # csrc/peerbuf.cpp's second round, one process per rank, no GPU (synthetic buffers): when a
     # call brings a buffer no read call used recently, every rank reports whether it could map
     # its peers' buffers before any launches; one failure (rank 1, call 3: an injected
     # hipIpcOpenMemHandle failure) -> the scratch schedule (0) for that call on EVERY rank and
     # the read schedule (1) on every other call; buffers reused call after call -> the round
-    # runs only for the calls that bring a new buffer.  dec[i] = decision + 10 x rounds so far.
+    # runs only for the calls that bring a new buffer; buffers reported freed by their owners ->
+    # every peer closes its mappings of them (1000 x closed).  dec[i] = decision + 10 x rounds so
+    # far.
     import gpu_workers as GW
     calls = 24
     port = GW.free_port()
@@ -122,6 +124,8 @@ def test_read_schedule_mapping_round(sim_lib, world, scenario):
         dec = out[r]["dec"]
         if scenario == 4:
             exp = [(0 if i == 2 else 1) + 10 * (i + 1) for i in range(calls)]
-        else:
+        elif scenario == 5:
             exp = [1 + 10 * (1 if i < calls // 2 else 2) for i in range(calls)]
+        else:  # the freed buffers' mappings closed on every peer (2 per peer), new ones mapped once
+            exp = [1 + 10 if i < calls // 2 else 1 + 20 + 1000 * 2 * (world - 1) for i in range(calls)]
         assert dec == exp, (r, dec)

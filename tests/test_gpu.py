@@ -71,9 +71,14 @@ def _run_allreduce(n, cases, env=None, timeout=300, barrier=True):
             assert res["bad"] == 0, f"rank {r} case {c}: {res['bad']} mismatches, first at {res['first']} {res.get('detail', '')}"
             assert res["async"] == 0
             # the read schedule ran (no fallback) whenever every rank's buffers are device memory
+            # from the caching allocator (fresh allocations may land on an address the process
+            # exported before: csrc/ipcreg.h refuses to share those, and the call falls back)
             dev_bufs = all(c.get(k, "device") == "device" for k in ("mem", "recv_mem"))
-            if c["algo"] == 2 and dev_bufs and c["count"] >= n:
+            if c["algo"] == 2 and dev_bufs and c["count"] >= n and not c.get("fresh"):
                 assert res["last_algo"] == 2, f"rank {r} case {c}: ran schedule {res['last_algo']}"
+            # no IPC open ever failed (nothing retries: a failure would send a call to the
+            # scratch schedule, csrc/peerbuf.cpp), in this process or in any rank's mapping round
+            assert res["ipc_open_failures"] == 0 and res["read_map_failures"] == 0, (r, c, res)
     return out
 
 
@@ -267,15 +272,45 @@ def test_read_schedule_count_mismatch_is_invalid_usage(dev):
 
 
 def test_read_schedule_allocation_churn(dev):
-    # a fresh send and recv allocation for each of 70 calls (each freed after its call, so
-    # addresses come back with new allocation ids): every call maps the peers' new
-    # allocations, the per-process mapping cache stays bounded (64, least recently used out)
-    # and no stale mapping of a re-used address is ever read -- bit-exact each time
-    cases = [_case(count=4099 + 13 * i, algo=2, seed=900 + i, inplace=(i % 3 == 0)) for i in range(70)]
-    out = _run_allreduce(2, cases, timeout=600)
-    for r in range(2):
-        assert all(res["peer_mappings"] <= 64 for res in out[r]["results"])
-        assert out[r]["results"][-1]["peer_mappings"] >= 2
+    # a fresh hipMalloc'd send and recv for each of 70 calls, freed after it (addresses come back
+    # with new allocation ids): an owner never shares an address it shared before (ROCm's IPC can
+    # then map another process's memory, profiles/r3_ipc_stress.txt), so such calls run the
+    # scratch schedule; every freed allocation a peer mapped is reported by its owner at its next
+    # call and the peer closes its import -- mappings stay bounded, no open fails, every call
+    # bit-exact
+    n = 3
+    cases = [_case(count=4099 + 13 * i, algo=2, seed=900 + i, inplace=(i % 3 == 0), fresh=True) for i in range(70)]
+    out = _run_allreduce(n, cases, timeout=600)
+    for r in range(n):
+        res = out[r]["results"]
+        assert res[0]["last_algo"] == 2  # the first allocations are new addresses: shared
+        # scratch + mailbox of each peer, plus at most the user allocations not yet reported freed
+        assert all(x["peer_mappings"] <= 2 * (n - 1) + 4 * (n - 1) for x in res), [x["peer_mappings"] for x in res]
+        assert res[-1]["closed_freed"] >= _freed_imports(res, n), [x["closed_freed"] for x in res]
+        assert all(x["live_exports"] <= 2 for x in res)
+
+
+def test_read_schedule_frees_mapped_allocations(dev):
+    # large allocations (64-96 MiB) mapped by every peer and then freed by their owner while the
+    # peers still hold the mappings (hipFree before the importers close: the owner reports the
+    # allocation freed with its next call, the peers close their imports then); new allocations
+    # of the same and other sizes after them -- every call bit-exact, no open fails, every freed
+    # allocation's imports closed
+    n = 3
+    sizes = [16 << 20, 16 << 20, 24 << 20, 16 << 20, 24 << 20, 20 << 20]  # elements (fp32)
+    cases = [_case(count=c + i, algo=2, seed=1300 + i, fresh=True, calls=2, vary=True) for i, c in enumerate(sizes)]
+    out = _run_allreduce(n, cases, timeout=600)
+    for r in range(n):
+        res = out[r]["results"]
+        assert res[0]["last_algo"] == 2
+        assert _freed_imports(res, n) >= 2 * (n - 1)
+        assert res[-1]["closed_freed"] >= _freed_imports(res, n), [x["closed_freed"] for x in res]
+
+
+def _freed_imports(res, n):
+    """imports a rank must have closed by the end: every peer buffer of every read case but the
+    last (an owner reports its freed allocations with its next call)"""
+    return sum((n - 1) * (1 if x["case"]["inplace"] else 2) for x in res[:-1] if x["last_algo"] == 2)
 
 
 @pytest.mark.parametrize("dtype,algos,gib,knobs", [

@@ -20,7 +20,7 @@ def test_host_logic_under_asan_ubsan(tmp_path):
     import gpu_workers as GW
     exe = str(tmp_path / "host_selftest")
     srcs = [os.path.join(ROOT, "tests", "native", "host_selftest.cpp")] + \
-        [os.path.join(CSRC, f) for f in ("sim.cpp", "bootstrap.cpp", "config.cpp", "peerbuf.cpp")]
+        [os.path.join(CSRC, f) for f in ("sim.cpp", "bootstrap.cpp", "config.cpp", "peerbuf.cpp", "ipcreg.cpp")]
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
            "-fno-sanitize-recover=undefined", "-pthread", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
            "-I" + CSRC, "-o", exe] + srcs + ["-L/opt/rocm/lib", "-lamdhip64", "-lrt", "-Wl,-rpath,/opt/rocm/lib"]
@@ -42,7 +42,7 @@ def _build_abi_selftest(tmp_path):
                        timeout=900)
     exe = str(tmp_path / "abi_selftest")
     srcs = [os.path.join(ROOT, "tests", "native", "abi_selftest.cpp")] + \
-        [os.path.join(CSRC, f) for f in ("api.cpp", "comm.cpp", "peerbuf.cpp", "bootstrap.cpp", "config.cpp")]
+        [os.path.join(CSRC, f) for f in ("api.cpp", "comm.cpp", "peerbuf.cpp", "ipcreg.cpp", "bootstrap.cpp", "config.cpp")]
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
            "-fno-sanitize-recover=undefined", "-Wno-unused-result", "-pthread", "-D__HIP_PLATFORM_AMD__",
            "-I/opt/rocm/include", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-o", exe] + srcs + \
