@@ -38,8 +38,7 @@ typedef enum {
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
   mncclAlgoDirect = 1, /* every peer pushes its slice of chunk c straight to rank c over its
                           own xGMI link; c folds them in ring order c, c+1, ..., c-1 and
-                          pushes the result to every peer (MINI_NCCL_ALGO=auto: from 3 ranks
-                          on, when the ranks are on more than one GPU) */
+                          pushes the result to every peer (only when chosen explicitly) */
   mncclAlgoRead = 2    /* no scratch: rank c loads the peers' slices of chunk c straight from
                           their send buffers (mapped per allocation, negotiated per call),
                           folds them in the same order into its recv, and every peer loads
@@ -74,8 +73,8 @@ typedef struct {
                              call some rank's buffers cannot take part in */
   size_t peer_mappings;   /* peer allocations mapped into this process (scratch, mailboxes and
                              read-schedule buffers of every communicator; csrc/ipcreg.h) */
-  int scratch_algo;       /* the read schedule's fallback (ring or direct), chosen from the
-                             ranks' GPUs: direct from 3 ranks on more than one GPU */
+  int scratch_algo;       /* the read schedule's fallback for calls whose buffers cannot be
+                             shared: the ring (direct only when forced by MINI_NCCL_ALGO) */
   int calib_choice;       /* MINI_NCCL_CALIBRATE: schedule kept for large calls (mncclAlgo_t), -1
                              while undecided or when calibration is off */
   double calib_ms[2];     /* the timings it was decided on: read, scratch schedule (ms per call,

@@ -225,20 +225,18 @@ void Comm::exchange_and_map() {
           "PIPE_DEPTH / DIRECT_OVERLAP / PULL / ALGO / TUNE / TUNE_BYTES / CALIBRATE / CALIBRATE_BYTES differ between "
           "ranks");
   }
-  // the scratch schedule of MINI_NCCL_ALGO=auto / read (the read schedule's fallback), the same
-  // on every rank (computed from the gathered records): from 3 ranks, `direct` when the ranks are
-  // on more than one GPU (each pair of an MI355X node has its own xGMI link; direct uses all of
-  // them, the ring one); `ring` when every rank shares one GPU (no links: the ring's
-  // neighbour-only coupling measured faster there, profiles/r2_direct_sweep_n4_same_gpu.txt)
-  // and at 2 ranks (one link either way)
+  // the scratch schedule of MINI_NCCL_ALGO=auto / read (the read schedule's fallback for calls
+  // whose buffers cannot be shared): the reference's ring, on every rank.  `direct` (every link
+  // at once) stays a forced choice (MINI_NCCL_ALGO=direct / mncclCommSetAlgo) until a node has
+  // measured it against the ring: on a shared GPU it trails the ring by 10-30 % with the same
+  // bytes (profiles/r3_direct_incremental_wait_ab.txt), and no cross-GPU run exists yet
   bool one_device = true;
   ranks_on_device_ = 0;
   for (int q = 0; q < nranks_; ++q) {
     if (all[(size_t)q].pci != all[0].pci) one_device = false;
     if (all[(size_t)q].pci == me.pci) ++ranks_on_device_;
   }
-  const int rule = (nranks_ >= 3 && !one_device) ? 1 : 0;
-  if (cfg_.algo < 0 || cfg_.algo == 2) scratch_algo_ = rule;
+  if (cfg_.algo < 0 || cfg_.algo == 2) scratch_algo_ = 0;
   // measured choice between read and the scratch schedule for large calls: by default where the
   // links decide it (ranks on more than one GPU); on one GPU read always wins (it moves half the
   // HBM bytes), so it is off there unless MINI_NCCL_CALIBRATE=1

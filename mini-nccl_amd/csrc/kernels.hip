@@ -472,11 +472,23 @@ constexpr int kFoldU = MNCCL_FOLD_U;  // vectors per lane per batch in the fold 
 
 // Fold of the n-1 arriving slices of this rank's own chunk, software-pipelined by one
 // peer so two slot loads per vector are in flight; acc = op(x_q, acc) in ring order.
-// rx0[q]: sequence number of q's raw message for this slice; tx1[d]: of my result message to d
+// rx0[q]: sequence number of q's raw message for this slice; tx1[d]: of my result message to d.
+// The peers' READY words are awaited here, one peer at a time in ring order, just before the
+// first loads of that peer's slice: the fold of the first arrivals overlaps the wait for the
+// later ones (a slice waited for all n-1 hand-offs before any work: the direct schedule's gap to
+// the ring on a shared GPU, profiles/r2_direct_sweep_n4_same_gpu.txt).  False: aborted.
 template <typename T, int OPC, bool VEC>
-__device__ __forceinline__ void fold_and_push(const CollParams& p, const char* lsrc, char* ldst, const u64* rx0,
-                                              const u64* tx1, uint32_t nbytes, int w, int C, int lane) {
+__device__ __forceinline__ bool fold_and_push(const CollParams& p, const Ctl& ctl, const char* lsrc, char* ldst,
+                                              const u64* rx0, const u64* tx1, uint32_t nbytes, int w, int C,
+                                              int lane) {
   const int n = p.n, r = p.rank;
+  auto ready = [&](int k) {
+    const int q = direct_peer(n, r, k);
+    if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 1, ctl, lane)) return false;
+    acquire_sys(p.sys_fence);
+    return true;
+  };
+  int waited = 0;  // peers (in ring order) whose READY has been seen
   if (VEC) {
     constexpr int U = kFoldU;
     const uint32_t nvec = nbytes >> 4;
@@ -487,6 +499,10 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
       v4u acc[U], cur[U], nxt[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u] = ld_g16(lsrc + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16);
+      if (waited < 1) {
+        if (!ready(1)) return false;
+        waited = 1;
+      }
       {
         const int q = direct_peer(n, r, 1);
         const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q]), nbytes);
@@ -495,6 +511,10 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
       }
       for (int k = 1; k < n; ++k) {
         if (k + 1 < n) {
+          if (waited < k + 1) {
+            if (!ready(k + 1)) return false;
+            waited = k + 1;
+          }
           const int q = direct_peer(n, r, k + 1);
           const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q]), nbytes);
 #pragma unroll
@@ -514,7 +534,9 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
         for (int u = 0; u < U; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
       }
     }
-    // the rest: one vector per lane
+    // the rest: one vector per lane (every peer's READY first)
+    for (; waited < n - 1; ++waited)
+      if (!ready(waited + 1)) return false;
     for (uint32_t i = b + (uint32_t)lane; i < nvec; i += 64) {
       v4u acc = ld_g16(lsrc + (size_t)i * 16);
       for (int k = 1; k < n; ++k) {
@@ -531,8 +553,11 @@ __device__ __forceinline__ void fold_and_push(const CollParams& p, const char* l
     }
     if (nbytes & 15u) fold_scalar<T, OPC>(p, lsrc, ldst, rx0, tx1, nbytes, w, C, lane, nvec * 16);
   } else {
+    for (; waited < n - 1; ++waited)
+      if (!ready(waited + 1)) return false;
     fold_scalar<T, OPC>(p, lsrc, ldst, rx0, tx1, nbytes, w, C, lane, 0);
   }
+  return true;
 }
 
 constexpr int kMaxWaves = kMaxThreads / 64;
@@ -609,18 +634,23 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) direct_kernel(C
         }
       }
     } else if (phase == 1) {
-      // Phase B: wait for the n-1 raw slices of my chunk and for slot credits of the
-      // result message at every peer; fold; store; push the result everywhere.
+      // Phase B: slot credits of the result message at every peer; then the fold, which waits
+      // for the n-1 raw slices of my chunk one peer at a time as it reaches them; store; push
+      // the result everywhere.
       for (int k = 1; k < n; ++k) {
         const int q = direct_peer(n, r, k);
-        if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 1, ctl, lane)) goto aborted;
         if (tx1[q] + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, q, w), tx1[q] + 1 - K, ctl, lane))
           goto aborted;
       }
-      acquire_sys(p.sys_fence);
       if (len) {
         const u64 coff = (u64)r * p.chunk_bytes + soff;
-        fold_and_push<T, OPC, VEC>(p, p.send + coff, p.recv + coff, rx0, tx1, len, w, C, lane);
+        if (!fold_and_push<T, OPC, VEC>(p, ctl, p.send + coff, p.recv + coff, rx0, tx1, len, w, C, lane))
+          goto aborted;
+      } else {
+        for (int k = 1; k < n; ++k) {  // an empty slice still consumes every peer's message
+          const int q = direct_peer(n, r, k);
+          if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 1, ctl, lane)) goto aborted;
+        }
       }
       drain_stores();
       if (lane == 0) {
@@ -636,15 +666,13 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) direct_kernel(C
         }
       }
     } else {
-      // Phase C: wait for every peer's result slice, store them all, one drain, n-1 credits
+      // Phase C: every peer's result slice, each copied as soon as its READY is seen (ring
+      // order), one drain, n-1 credits
       for (int k = 1; k < n; ++k) {
         const int q = direct_peer(n, r, k);
         if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 2, ctl, lane)) goto aborted;
-      }
-      acquire_sys(p.sys_fence);
-      if (len) {
-        for (int k = 1; k < n; ++k) {
-          const int q = direct_peer(n, r, k);
+        acquire_sys(p.sys_fence);
+        if (len) {
           const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q] + 1), len);
           const u64 coff = (u64)q * p.chunk_bytes + soff;
           move<T, OPC, VEC, kCopy>(nullptr, p.recv + coff, in, in, len, lane);
