@@ -16,6 +16,12 @@
 // Device: rank % device_count (the reference pinned every rank to GPU 0, :46;
 // MINI_NCCL_PERF_DEVICE overrides).
 #include <hip/hip_runtime.h>
+
+#include "mini_nccl_ext.h"  // mncclCommGetInfoV: which schedule each size ran (diagnostic column)
+
+// weak: the program also runs against a library without it (an older build, or another
+// implementation of the ABI), and prints "?" there
+extern "C" ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* info, size_t size) __attribute__((weak));
 #include <immintrin.h>
 #include <time.h>
 #include <unistd.h>
@@ -104,7 +110,7 @@ int main(int argc, char** argv) {
   if (rank == 0) {
     printf("\n=== Mini-NCCL (MI355X) Performance Benchmark, %d ranks, %s buffers ===\n", nranks,
            mode == "device" ? "HBM-resident" : mode == "host" ? "pinned host buffers passed to ncclAllReduce" : "host-staged (H2D + all-reduce + D2H)");
-    printf("%15s %15s %15s %15s\n", "Size(B)", "Time(us)", "AlgBW(GB/s)", "BusBW(GB/s)");
+    printf("%15s %15s %15s %15s %9s\n", "Size(B)", "Time(us)", "AlgBW(GB/s)", "BusBW(GB/s)", "Schedule");
   }
   int failures = 0;
   for (size_t bytes : sizes) {
@@ -148,7 +154,11 @@ int main(int argc, char** argv) {
     const double us = (t1 - t0) / iters;
     const double alg = (double)bytes / us / 1e3;
     const double bus = alg * 2.0 * (nranks - 1) / nranks;
-    if (rank == 0) printf("%15zu %15.2f %15.2f %15.2f %s\n", bytes, us, alg, bus, bad >= 0 ? "(FAIL)" : "");
+    mncclCommInfo_t info;
+    memset(&info, 0, sizeof info);
+    const char* sched = !mncclCommGetInfoV || mncclCommGetInfoV(comm, &info, sizeof info) != ncclSuccess ? "?"
+                        : info.last_algo == 0 ? "ring" : info.last_algo == 1 ? "direct" : info.last_algo == 2 ? "read" : "-";
+    if (rank == 0) printf("%15zu %15.2f %15.2f %15.2f %9s %s\n", bytes, us, alg, bus, sched, bad >= 0 ? "(FAIL)" : "");
     fflush(stdout);
     HIP_OK(hipFree(d_send));
     HIP_OK(hipFree(d_recv));

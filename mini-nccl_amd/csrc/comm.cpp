@@ -610,8 +610,14 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     // through a device staging copy.  Every rank launches the same kernel either way.
     const void* ksend = send;
     void* krecv = recv;
+    // buffers the read schedule already shares (live exports of this process, checked by reap())
+    // need no pointer query: device memory of this GPU
     bool local_s = false, local_r = false;
-    const Reach rs = reach(send, &ksend, &local_s), rr = reach(recv, (const void**)&krecv, &local_r);
+    const bool read_sched = algo_ == 2 && pbuf_.available();
+    if (read_sched) pbuf_.reap();
+    const Reach rs = read_sched && pbuf_.known(send) ? (local_s = true, Reach::kDevice) : reach(send, &ksend, &local_s);
+    const Reach rr = read_sched && pbuf_.known(recv) ? (local_r = true, Reach::kDevice)
+                                                     : reach(recv, (const void**)&krecv, &local_r);
     if (rs == Reach::kStaged || rr == Reach::kStaged) {
       if (cap != hipStreamCaptureStatusNone) {
         fprintf(stderr, "[Mini-NCCL] pageable host buffers cannot be captured into a HIP graph\n");

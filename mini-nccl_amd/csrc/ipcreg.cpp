@@ -14,7 +14,7 @@ namespace ipc {
 namespace {
 
 struct Export {
-  uint64_t base, id;
+  uint64_t base, id, size;
   hipIpcMemHandle_t h;
 };
 struct Import {
@@ -40,6 +40,7 @@ struct KeyHash {
 struct State {
   std::mutex mu;
   std::vector<Export> exports;            // live exports
+  std::vector<std::pair<uint64_t, uint64_t>> freed;  // exports found freed, in order
   std::unordered_set<uint64_t> exported;  // every address ever exported or tried (never again for another id)
   std::vector<Import> imports;
   std::unordered_set<Key, KeyHash> closed;  // imports closed: never re-opened
@@ -54,7 +55,20 @@ State& st() {
 
 }  // namespace
 
-bool export_allocation(uint64_t base, uint64_t id, hipIpcMemHandle_t* h) {
+bool find_live_export(uint64_t p, uint64_t* base, uint64_t* id, hipIpcMemHandle_t* h) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  for (const Export& e : s.exports)
+    if (p >= e.base && p - e.base < e.size) {
+      *base = e.base;
+      *id = e.id;
+      *h = e.h;
+      return true;
+    }
+  return false;
+}
+
+bool export_allocation(uint64_t base, uint64_t id, uint64_t size, hipIpcMemHandle_t* h) {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
   for (const Export& e : s.exports)
@@ -67,26 +81,36 @@ bool export_allocation(uint64_t base, uint64_t id, hipIpcMemHandle_t* h) {
     (void)hipGetLastError();
     return false;  // the address stays marked: never tried again
   }
-  s.exports.push_back(Export{base, id, *h});
+  s.exports.push_back(Export{base, id, size, *h});
   return true;
 }
 
-std::vector<std::pair<uint64_t, uint64_t>> reap_freed_exports() {
+size_t freed_log_size() {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
-  std::vector<std::pair<uint64_t, uint64_t>> out;
+  return s.freed.size();
+}
+
+std::pair<uint64_t, uint64_t> freed_log_at(size_t i) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  return s.freed.at(i);
+}
+
+void reap_freed_exports() {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
   for (size_t i = 0; i < s.exports.size();) {
     unsigned long long id = 0;
     const hipError_t e = hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)s.exports[i].base);
     if (e != hipSuccess || id != s.exports[i].id) {
       (void)hipGetLastError();
-      out.emplace_back(s.exports[i].base, s.exports[i].id);
+      s.freed.emplace_back(s.exports[i].base, s.exports[i].id);
       s.exports.erase(s.exports.begin() + (long)i);
     } else {
       ++i;
     }
   }
-  return out;
 }
 
 size_t live_exports() {

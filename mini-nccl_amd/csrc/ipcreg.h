@@ -32,10 +32,17 @@ namespace ipc {
 // The handle of allocation (base, id); exported on first use.  False (no handle) when the
 // address was exported before for another allocation, or the export fails: such a buffer
 // cannot be shared safely and its calls run a scratch schedule.
-bool export_allocation(uint64_t base, uint64_t id, hipIpcMemHandle_t* h);
-// Exports whose allocation has been freed since the last call (base, id), removed from the live
-// list; their addresses are never exported again.
-std::vector<std::pair<uint64_t, uint64_t>> reap_freed_exports();
+bool export_allocation(uint64_t base, uint64_t id, uint64_t size, hipIpcMemHandle_t* h);
+// A live export (as of the last reap_freed_exports) holding address p: its base, id and handle,
+// with no HIP call (a caller that reuses its buffers pays no pointer queries per call).
+bool find_live_export(uint64_t p, uint64_t* base, uint64_t* id, hipIpcMemHandle_t* h);
+// Finds the exports whose allocation has been freed (one pointer query per live export), moves
+// them from the live list to the process's freed log; their addresses are never exported again.
+void reap_freed_exports();
+// The freed log (base, id), append-only: every communicator of the process reads it from its
+// own cursor (any of them may have shared the allocation with its peers).
+size_t freed_log_size();
+std::pair<uint64_t, uint64_t> freed_log_at(size_t i);
 size_t live_exports();
 
 // --- imports (peers' allocations), keyed by the owner's process nonce and (base, id)

@@ -90,6 +90,7 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
     (void)hipGetLastError();
     device_ = -1;
   }
+  if (!test_fake_) freed_cursor_ = ipc::freed_log_size();  // earlier frees: earlier communicators' business
   board_bytes_ = (sizeof(Board) + 4095) & ~(size_t)4095;
   // rank 0 creates the segment under a name unique to this communicator and shares it; every
   // rank maps it; once all have, rank 0 unlinks it (nothing is left in /dev/shm, even if a
@@ -145,6 +146,21 @@ void PeerBuffers::lock() {
 
 void PeerBuffers::unlock() { pthread_mutex_unlock(&board_->ipc_lock); }
 
+void PeerBuffers::reap() {
+  // allocations this process exported and has freed since my last call: my peers close their
+  // imports (the process's log: another communicator of this process may have found them)
+  if (test_fake_) return;
+  ipc::reap_freed_exports();
+  for (const size_t end = ipc::freed_log_size(); freed_cursor_ < end; ++freed_cursor_)
+    freed_.push_back(ipc::freed_log_at(freed_cursor_));
+}
+
+bool PeerBuffers::known(const void* p) const {
+  uint64_t b = 0, i = 0;
+  hipIpcMemHandle_t h;
+  return !test_fake_ && ipc::find_live_export((uint64_t)(uintptr_t)p, &b, &i, &h);
+}
+
 size_t PeerBuffers::mapped_allocations() const { return test_fake_ ? fake_maps_.size() : ipc::imports(); }
 
 // (base, id, handle) of the allocation holding p, exported once; false: it cannot be shared
@@ -156,17 +172,20 @@ bool PeerBuffers::describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMe
     memset(h, 0, sizeof *h);
     return true;
   }
+  if (ipc::find_live_export((uint64_t)(uintptr_t)p, base, id, h)) return true;  // checked alive by reap()
   hipDeviceptr_t b = 0;
+  size_t sz = 0;
   unsigned long long bid = 0;
-  hipPointer_attribute attrs[2] = {HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, HIP_POINTER_ATTRIBUTE_BUFFER_ID};
-  void* vals[2] = {&b, &bid};
-  if (hipDrvPointerGetAttributes(2, attrs, vals, (hipDeviceptr_t)p) != hipSuccess || !b) {
+  hipPointer_attribute attrs[3] = {HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
+                                   HIP_POINTER_ATTRIBUTE_BUFFER_ID};
+  void* vals[3] = {&b, &sz, &bid};
+  if (hipDrvPointerGetAttributes(3, attrs, vals, (hipDeviceptr_t)p) != hipSuccess || !b || !sz) {
     (void)hipGetLastError();
     return false;
   }
   *base = (uint64_t)(uintptr_t)b;
   *id = bid;
-  return ipc::export_allocation(*base, bid, h);
+  return ipc::export_allocation(*base, bid, sz, h);
 }
 
 // rank q's allocation (base, id) mapped here; nullptr (and *why) if it cannot be.  Caller holds
@@ -239,10 +258,6 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
   if (k > (uint64_t)kBoardDepth)
     for (int q = 0; q < nranks_; ++q)
       if (q != rank_) wait(board_->consumed[q].v, k - kBoardDepth, q, "finish reading the records before");
-
-  // allocations I exported and have freed since my last call: my peers close their imports
-  if (!test_fake_)
-    for (const auto& f : ipc::reap_freed_exports()) freed_.push_back(f);
 
   CallRec& me = board_->rec[rank_][slot];
   BufDesc sd, rd;

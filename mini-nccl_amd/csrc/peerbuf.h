@@ -64,6 +64,13 @@ class PeerBuffers {
                      double timeout_s, const std::function<void()>& sync_previous, const char** psend,
                      const char** precv, bool* vec_all, const float* my_t = nullptr, float* max_t = nullptr);
 
+  // This rank's exported allocations freed since the last call are found (one pointer query per
+  // live export) and queued for its next record.  Call before known() in each call.
+  void reap();
+  // p lies in one of this rank's live exported allocations (no HIP call): device memory of
+  // this GPU that the read schedule can share
+  bool known(const void* p) const;
+
   // for tests / diagnostics
   size_t mapped_allocations() const;                    // peer allocations mapped in this process
   uint64_t agreements() const { return agreements_; }  // calls that needed the mapping round
@@ -97,6 +104,7 @@ class PeerBuffers {
   uint64_t seq_ = 0;  // calls negotiated so far
   // allocations this rank exported and has since freed, not yet published
   std::deque<std::pair<uint64_t, uint64_t>> freed_;
+  size_t freed_cursor_ = 0;  // next entry of the process's freed log (ipcreg.h) to publish
   // (rank, base, id) of every buffer a read call ran on and no owner has reported freed since:
   // every rank still maps them (imports stay open until then), so a call whose buffers are all
   // here needs no mapping round.  Derived from the records alone: the same on every rank.
