@@ -173,13 +173,13 @@ bool PeerBuffers::describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMe
     return true;
   }
   if (ipc::find_live_export((uint64_t)(uintptr_t)p, base, id, h)) return true;  // checked alive by reap()
+  // a new allocation (once per allocation): its range and id.  Not HIP_POINTER_ATTRIBUTE_RANGE_SIZE:
+  // it comes back truncated to 32 bits (0 for a 4 GiB allocation on ROCm 7.2)
   hipDeviceptr_t b = 0;
   size_t sz = 0;
   unsigned long long bid = 0;
-  hipPointer_attribute attrs[3] = {HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
-                                   HIP_POINTER_ATTRIBUTE_BUFFER_ID};
-  void* vals[3] = {&b, &sz, &bid};
-  if (hipDrvPointerGetAttributes(3, attrs, vals, (hipDeviceptr_t)p) != hipSuccess || !b || !sz) {
+  if (hipMemGetAddressRange(&b, &sz, (hipDeviceptr_t)p) != hipSuccess || !b || !sz ||
+      hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
