@@ -133,6 +133,9 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
   for (int v : oks) all = all && v;
   if (!all) {
     if (m != MAP_FAILED) munmap(m, board_bytes_);
+    if (rank == 0)
+      fprintf(stderr, "[Mini-NCCL] warning: the ranks share no /dev/shm (per-call records): the read schedule is off "
+              "and every call runs the ring\n");
     return;  // no board anywhere: the read schedule falls back on every rank
   }
   board_ = static_cast<Board*>(m);
