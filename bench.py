@@ -905,7 +905,12 @@ def main():
         # each schedule's ceiling from the probed links (min over ranks): the ring moves
         # 2(n-1)/n of the buffer through one link, direct 2/n through each of n-1 links as
         # stores, read the same 2/n per link as loads (the probe's mesh pull from user memory)
-        if "probe_next_GBps" in link:
+        if args.same_device:
+            # every "link" of the one-GPU rehearsal is this GPU's HBM, shared with the other ranks'
+            # kernels: a schedule's rate over that is no link fraction (round 2 printed 1.43)
+            link["frac"] = None
+            link["note"] = "ranks share one GPU: the probes measure its HBM, not xGMI; no link fractions"
+        elif "probe_next_GBps" in link:
             pv = link.get("probe_variants_GBps_per_link", {})
             pull = pv.get("mesh_pull_sys_user") or pv.get("mesh_pull_sys")
             ceil = {"ring": link["probe_next_GBps"] * n / (2 * (n - 1)),
