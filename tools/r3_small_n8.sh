@@ -1,0 +1,22 @@
+#!/bin/bash
+# Small-call time at 2 / 4 / 8 ranks sharing one GPU, ring vs read (perf_test rank 0, 200 calls
+# per size): is the 8-rank floor the read schedule's host rendezvous or the shared GPU?
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+export GPU_MAX_HW_QUEUES=2 MINI_NCCL_PERF_DEVICE=0
+for nr in 2 4 8; do
+  for algo in ring read; do
+    port=$((21000 + RANDOM % 20000))
+    pids=()
+    for ((r = 1; r < nr; r++)); do
+      MINI_NCCL_ALGO=$algo MINI_NCCL_PORT=$port timeout -k 5 120 $R/apps/bin/perf_test $r $nr --sizes 4k,64k,1 --iters 200 > /tmp/sn_$r.log 2>&1 &
+      pids+=($!)
+    done
+    MINI_NCCL_ALGO=$algo MINI_NCCL_PORT=$port timeout -k 5 120 $R/apps/bin/perf_test 0 $nr --sizes 4k,64k,1 --iters 200 > /tmp/sn_0.log 2>&1
+    rc=$?
+    for p in "${pids[@]}"; do wait $p; done
+    echo "== n=$nr algo=$algo rc=$rc"
+    grep -E "^ +[0-9]+ " /tmp/sn_0.log
+    [ $rc -ne 0 ] && exit 9
+  done
+done
+exit 0
