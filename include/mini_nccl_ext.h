@@ -71,8 +71,8 @@ typedef struct {
   int last_algo;          /* schedule the last all-reduce ran (mncclAlgo_t; -1: no kernel
                              yet): mncclAlgoRead falls back to the scratch schedule for a
                              call some rank's buffers cannot take part in */
-  size_t peer_mappings;   /* peer allocations mapped into this process (scratch, mailboxes and
-                             read-schedule buffers of every communicator; csrc/ipcreg.h) */
+  size_t peer_mappings;   /* peers' user allocations mapped into this process for the read
+                             schedule (dma-buf imports of every communicator; csrc/ipcreg.h) */
   int scratch_algo;       /* the read schedule's fallback for calls whose buffers cannot be
                              shared: the ring (direct only when forced by MINI_NCCL_ALGO) */
   int calib_choice;       /* MINI_NCCL_CALIBRATE: schedule kept for large calls (mncclAlgo_t), -1
@@ -80,7 +80,7 @@ typedef struct {
   double calib_ms[2];     /* the timings it was decided on: read, scratch schedule (ms per call,
                              max over ranks); 0 until decided */
   /* since 300 */
-  unsigned long long ipc_open_failures;  /* hipIpcOpenMemHandle failures in this process */
+  unsigned long long ipc_open_failures;  /* user-buffer imports that failed in this process */
   unsigned long long read_map_failures;  /* read calls this rank could not map (call fell back) */
   unsigned long long read_rounds;        /* read calls that needed the mapping round */
   unsigned long long closed_freed;       /* imports closed because their owner freed them */

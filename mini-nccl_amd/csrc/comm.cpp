@@ -286,9 +286,9 @@ void Comm::exchange_and_map() {
     // through the process's import registry: a peer block this process imported for an earlier
     // communicator is still mapped (imports of pool blocks are never closed, ipcreg.h)
     hipError_t e = hipSuccess;
-    char* ps = ipc::open_import(p.nonce, p.scratch_ptr, p.scratch_id, p.scratch_h, &e);
+    char* ps = ipc::open_block(p.nonce, p.scratch_ptr, p.scratch_id, p.scratch_h, &e);
     hip_check(ps ? hipSuccess : e, "ipc open scratch");
-    char* pm = ipc::open_import(p.nonce, p.mbox_ptr, p.mbox_id, p.mbox_h, &e);
+    char* pm = ipc::open_block(p.nonce, p.mbox_ptr, p.mbox_id, p.mbox_h, &e);
     hip_check(pm ? hipSuccess : e, "ipc open mailbox");
     peer_scratch_[(size_t)q] = ps;
     peer_mbox_[(size_t)q] = (uint64_t*)pm;
@@ -803,7 +803,7 @@ ncclResult_t Comm::link_probe(int all_peers, size_t bytes, int iters, double* gb
         continue;
       }
       hipError_t e = hipSuccess;
-      opened[(size_t)q] = ipc::open_import(u.nonce, u.base, u.id, u.h, &e);
+      opened[(size_t)q] = ipc::open_block(u.nonce, u.base, u.id, u.h, &e);
       hip_check(opened[(size_t)q] ? hipSuccess : e, "probe ipc open");
     }
   }

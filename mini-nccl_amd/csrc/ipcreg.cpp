@@ -1,23 +1,36 @@
 // ipcreg.cpp -- see ipcreg.h.
 #include "ipcreg.h"
 
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <cstdio>
+#include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <string>
-#include <unordered_set>
 
 namespace mnccl {
 namespace ipc {
 
 namespace {
 
+constexpr size_t kMaxExports = 512;  // descriptors this process holds open for its peers
+
 struct Export {
   uint64_t base, id, size;
-  hipIpcMemHandle_t h;
+  Shared d;
 };
 struct Import {
+  uint64_t owner, base, id;
+  void* map;    // the dma-buf's mapping (unmapped on close)
+  char* local;  // map + the owner's bo_off: the owner's base
+};
+struct BlockImport {
   uint64_t owner, base, id;
   char* local;
 };
@@ -29,22 +42,15 @@ struct Block {
   hipIpcMemHandle_t h;
   bool busy;
 };
-struct Key {
-  uint64_t owner, base, id;
-  bool operator==(const Key& o) const { return owner == o.owner && base == o.base && id == o.id; }
-};
-struct KeyHash {
-  size_t operator()(const Key& k) const { return std::hash<uint64_t>{}(k.owner * 0x9E3779B97F4A7C15ull ^ k.base ^ (k.id << 17)); }
-};
 
 struct State {
   std::mutex mu;
-  std::vector<Export> exports;            // live exports
+  std::vector<Export> exports;                       // live exports
   std::vector<std::pair<uint64_t, uint64_t>> freed;  // exports found freed, in order
-  std::unordered_set<uint64_t> exported;  // every address ever exported or tried (never again for another id)
   std::vector<Import> imports;
-  std::unordered_set<Key, KeyHash> closed;  // imports closed: never re-opened
+  std::vector<BlockImport> blocks;
   std::vector<Block> pool;
+  std::vector<std::pair<int, hsa_agent_t>> agents;  // HIP device ordinal -> its HSA agent
   uint64_t open_failures = 0;
 };
 
@@ -53,35 +59,129 @@ State& st() {
   return *s;
 }
 
+std::string err_str(const char* what, hsa_status_t e) {
+  const char* m = nullptr;
+  if (hsa_status_string(e, &m) != HSA_STATUS_SUCCESS || !m) m = "unknown status";
+  char b[256];
+  snprintf(b, sizeof b, "%s: HSA status 0x%x (%s)", what, (unsigned)e, m);
+  return b;
+}
+
+struct AgentMatch {
+  uint32_t domain, bdf;
+  hsa_agent_t found;
+};
+
+hsa_status_t match_agent(hsa_agent_t a, void* arg) {
+  AgentMatch* m = static_cast<AgentMatch*>(arg);
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+    return HSA_STATUS_SUCCESS;
+  uint32_t bdf = 0, dom = 0;
+  if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) != HSA_STATUS_SUCCESS ||
+      hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) != HSA_STATUS_SUCCESS)
+    return HSA_STATUS_SUCCESS;
+  // BDFID = bus << 8 | device << 3 | function; HIP reports bus and device
+  if (dom == m->domain && (bdf >> 3) == (m->bdf >> 3)) {
+    m->found = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// The HSA agent of this thread's current HIP device (HIP runs on the same runtime).  Caller holds
+// s.mu.
+bool current_agent(State& s, hsa_agent_t* out, std::string* why) {
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    *why = "hipGetDevice failed";
+    return false;
+  }
+  for (const auto& a : s.agents)
+    if (a.first == dev) {
+      *out = a.second;
+      return true;
+    }
+  int dom = 0, bus = 0, devno = 0;
+  if (hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, dev) != hipSuccess ||
+      hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dev) != hipSuccess ||
+      hipDeviceGetAttribute(&devno, hipDeviceAttributePciDeviceId, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    *why = "PCI location of the current device unknown";
+    return false;
+  }
+  AgentMatch m{(uint32_t)dom, (uint32_t)((bus << 8) | (devno << 3)), hsa_agent_t{0}};
+  // HIP has brought the runtime up (the device is in use); only if it has not, take a reference
+  // of our own (never released: HIP's shutdown then leaves the runtime to the process exit)
+  if (hsa_iterate_agents(match_agent, &m) == HSA_STATUS_ERROR_NOT_INITIALIZED) {
+    const hsa_status_t e = hsa_init();
+    if (e != HSA_STATUS_SUCCESS) {
+      *why = err_str("hsa_init", e);
+      return false;
+    }
+    hsa_iterate_agents(match_agent, &m);
+  }
+  if (!m.found.handle) {
+    *why = "no HSA agent at the current device's PCI location";
+    return false;
+  }
+  s.agents.emplace_back(dev, m.found);
+  *out = m.found;
+  return true;
+}
+
 }  // namespace
 
-bool find_live_export(uint64_t p, uint64_t* base, uint64_t* id, hipIpcMemHandle_t* h) {
+bool find_live_export(uint64_t p, uint64_t* base, uint64_t* id, Shared* d) {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
   for (const Export& e : s.exports)
     if (p >= e.base && p - e.base < e.size) {
       *base = e.base;
       *id = e.id;
-      *h = e.h;
+      *d = e.d;
       return true;
     }
   return false;
 }
 
-bool export_allocation(uint64_t base, uint64_t id, uint64_t size, hipIpcMemHandle_t* h) {
+bool export_allocation(uint64_t base, uint64_t id, uint64_t size, Shared* d, std::string* why) {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
   for (const Export& e : s.exports)
     if (e.base == base && e.id == id) {
-      *h = e.h;
+      *d = e.d;
       return true;
     }
-  if (!s.exported.insert(base).second) return false;  // this address was exported before (another allocation)
-  if (hipIpcGetMemHandle(h, (void*)(uintptr_t)base) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;  // the address stays marked: never tried again
+  std::string w;
+  hsa_agent_t a;
+  if (!current_agent(s, &a, &w)) {  // also brings HSA up
+    if (why) *why = w;
+    return false;
   }
-  s.exports.push_back(Export{base, id, size, *h});
+  if (s.exports.size() >= kMaxExports) {
+    if (why) *why = "this process holds " + std::to_string(kMaxExports) + " exports already";
+    return false;
+  }
+  int fd = -1;
+  uint64_t off = 0;
+  const hsa_status_t e = hsa_amd_portable_export_dmabuf((const void*)(uintptr_t)base, size, &fd, &off);
+  if (e != HSA_STATUS_SUCCESS) {
+    if (why) *why = err_str("hsa_amd_portable_export_dmabuf", e);
+    return false;
+  }
+  struct stat sb;
+  if (fstat(fd, &sb) != 0) {
+    hsa_amd_portable_close_dmabuf(fd);
+    if (why) *why = std::string("fstat of an exported dma-buf: ") + strerror(errno);
+    return false;
+  }
+  d->fd = fd;
+  d->pad = 0;
+  d->ino = (uint64_t)sb.st_ino;
+  d->bo_off = off;
+  s.exports.push_back(Export{base, id, size, *d});
   return true;
 }
 
@@ -105,6 +205,8 @@ void reap_freed_exports() {
     const hipError_t e = hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)s.exports[i].base);
     if (e != hipSuccess || id != s.exports[i].id) {
       (void)hipGetLastError();
+      // the peers' imports hold their own references: closing ours releases nothing they use
+      hsa_amd_portable_close_dmabuf(s.exports[i].d.fd);
       s.freed.emplace_back(s.exports[i].base, s.exports[i].id);
       s.exports.erase(s.exports.begin() + (long)i);
     } else {
@@ -127,25 +229,41 @@ char* find_import(uint64_t owner, uint64_t base, uint64_t id) {
   return nullptr;
 }
 
-char* open_import(uint64_t owner, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h, hipError_t* err) {
+char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shared& d, std::string* why) {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
   for (const Import& m : s.imports)
-    if (m.owner == owner && m.base == base && m.id == id) return m.local;
-  if (s.closed.count(Key{owner, base, id})) {
-    *err = hipErrorInvalidValue;  // re-opening a closed import can map the wrong memory
-    return nullptr;
-  }
-  void* p = nullptr;
-  const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
+    if (m.owner == owner && m.base == base && m.id == id) {
+      if (fd >= 0) close(fd);
+      return m.local;
+    }
+  auto fail = [&](const std::string& w) -> char* {
+    if (fd >= 0) close(fd);
     ++s.open_failures;
-    *err = e;
+    *why = w;
+    return nullptr;
+  };
+  if (fd < 0) return fail("no descriptor arrived from the owner");
+  hsa_agent_t agent;
+  std::string w;
+  if (!current_agent(s, &agent, &w)) return fail(w);
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || (uint64_t)sb.st_ino != d.ino)
+    return fail("the received descriptor does not name the exported dma-buf");
+  size_t sz = 0;
+  void* p = nullptr;
+  const hsa_status_t e = hsa_amd_interop_map_buffer(1, &agent, (hsa_handle_t)fd, 0, &sz, &p, nullptr, nullptr);
+  if (e != HSA_STATUS_SUCCESS) return fail(err_str("hsa_amd_interop_map_buffer", e));
+  close(fd);  // the mapping holds its own reference
+  if (d.bo_off >= sz) {
+    hsa_amd_interop_unmap_buffer(p);
+    ++s.open_failures;
+    *why = "an exported allocation lies outside its dma-buf";
     return nullptr;
   }
-  s.imports.push_back(Import{owner, base, id, (char*)p});
-  return (char*)p;
+  char* local = (char*)p + d.bo_off;
+  s.imports.push_back(Import{owner, base, id, p, local});
+  return local;
 }
 
 bool close_import(uint64_t owner, uint64_t base, uint64_t id) {
@@ -153,10 +271,8 @@ bool close_import(uint64_t owner, uint64_t base, uint64_t id) {
   std::lock_guard<std::mutex> g(s.mu);
   for (size_t i = 0; i < s.imports.size(); ++i)
     if (s.imports[i].owner == owner && s.imports[i].base == base && s.imports[i].id == id) {
-      (void)hipIpcCloseMemHandle(s.imports[i].local);
-      (void)hipGetLastError();
+      hsa_amd_interop_unmap_buffer(s.imports[i].map);
       s.imports.erase(s.imports.begin() + (long)i);
-      s.closed.insert(Key{owner, base, id});
       return true;
     }
   return false;
@@ -192,20 +308,12 @@ void* pool_acquire(size_t bytes, unsigned flags, hipIpcMemHandle_t* h, uint64_t*
     return b.p;
   }
   void* p = nullptr;
-  for (int attempt = 0;; ++attempt) {
-    const hipError_t e = flags ? hipExtMallocWithFlags(&p, bytes, flags) : hipMalloc(&p, bytes);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      throw std::runtime_error(std::string("device allocation of ") + std::to_string(bytes) + " B: " +
-                               hipGetErrorString(e));
-    }
-    if (!s.exported.count((uint64_t)(uintptr_t)p)) break;
-    // an address this process exported before (a freed user buffer's): never export it again;
-    // keep the block out of use (freeing it would hand the same address back)
-    s.pool.push_back(Block{p, bytes, flags, 0, hipIpcMemHandle_t{}, true});
-    if (attempt == 3) throw std::runtime_error("device allocation: no address that was not exported before");
+  hipError_t e = flags ? hipExtMallocWithFlags(&p, bytes, flags) : hipMalloc(&p, bytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    throw std::runtime_error(std::string("device allocation of ") + std::to_string(bytes) + " B: " +
+                             hipGetErrorString(e));
   }
-  hipError_t e = hipSuccess;
   unsigned long long bid = 0;
   e = hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p);
   if (e == hipSuccess) e = hipIpcGetMemHandle(h, p);
@@ -214,7 +322,6 @@ void* pool_acquire(size_t bytes, unsigned flags, hipIpcMemHandle_t* h, uint64_t*
     (void)hipFree(p);
     throw std::runtime_error(std::string("IPC export of a communicator buffer: ") + hipGetErrorString(e));
   }
-  s.exported.insert((uint64_t)(uintptr_t)p);
   s.pool.push_back(Block{p, bytes, flags, bid, *h, true});
   *id = bid;
   return p;
@@ -226,6 +333,22 @@ void pool_release(void* p) {
   std::lock_guard<std::mutex> g(s.mu);
   for (Block& b : s.pool)
     if (b.p == p) b.busy = false;
+}
+
+char* open_block(uint64_t owner, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h, hipError_t* err) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  for (const BlockImport& m : s.blocks)
+    if (m.owner == owner && m.base == base && m.id == id) return m.local;
+  void* p = nullptr;
+  const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *err = e;
+    return nullptr;
+  }
+  s.blocks.push_back(BlockImport{owner, base, id, (char*)p});
+  return (char*)p;
 }
 
 }  // namespace ipc

@@ -3,9 +3,11 @@
 
 #include <errno.h>
 #include <fcntl.h>
-#include <pthread.h>
 #include <sched.h>
 #include <sys/mman.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/un.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -43,7 +45,7 @@ void backoff(int spins) {
 struct BufDesc {
   uint64_t base, id, off;  // allocation base / id in the owner's process, buffer - base
   uint64_t raw;            // the buffer's address in the owner's process (same-process peers)
-  hipIpcMemHandle_t h;     // of the allocation base
+  ipc::Shared d;           // the allocation's dma-buf export (ipcreg.h)
 };
 
 struct alignas(64) CallRec {
@@ -66,9 +68,6 @@ struct alignas(64) Counter {
 
 struct Board {
   uint32_t magic, nranks;
-  // serialises hipIpcOpenMemHandle / hipIpcCloseMemHandle across the ranks' processes (robust:
-  // a process that dies holding it does not block the others)
-  alignas(64) pthread_mutex_t ipc_lock;
   Counter consumed[kMaxRanks];  // last call whose records rank q has read
   Counter gave_up[kMaxRanks];   // != 0: rank q abandoned a rendezvous (its communicator is dead)
   CallRec rec[kMaxRanks][kBoardDepth];
@@ -76,10 +75,31 @@ struct Board {
 
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "the board needs address-free atomics");
 
+// A datagram carrying the descriptors of a rank's allocations that are new to the communicator
+// (SCM_RIGHTS: nfd descriptors, in the order of base / id).
+struct FdMsg {
+  uint64_t k;  // the call
+  int32_t src, nfd;
+  uint64_t base[2], id[2];
+};
+
 PeerBuffers::~PeerBuffers() {
   // imports stay open (ipcreg.h): a later communicator of this process reuses them
   if (board_) munmap(board_, board_bytes_);
   board_ = nullptr;
+  if (sock_ >= 0) close(sock_);
+  for (Pending& p : pending_)
+    for (int i = 0; i < p.nfd; ++i) close(p.fd[i]);
+  for (auto& f : fake_fds_) close(f.second);
+}
+
+void PeerBuffers::sock_addr(int q, void* addr, unsigned* len) const {
+  sockaddr_un* a = static_cast<sockaddr_un*>(addr);
+  memset(a, 0, sizeof *a);
+  a->sun_family = AF_UNIX;
+  // abstract namespace (leading NUL): nothing on the file system, gone with the socket
+  const int k = snprintf(a->sun_path + 1, sizeof a->sun_path - 1, "%s-r%d", sock_base_.c_str(), q);
+  *len = (unsigned)(offsetof(sockaddr_un, sun_path) + 1 + (size_t)k);
 }
 
 void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<uint64_t>& nonces, int port) {
@@ -119,12 +139,18 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
   int ok = m != MAP_FAILED ? 1 : 0;
   if (ok && rank == 0) {
     Board* b = static_cast<Board*>(m);
-    pthread_mutexattr_t a;
-    ok = pthread_mutexattr_init(&a) == 0 && pthread_mutexattr_setpshared(&a, PTHREAD_PROCESS_SHARED) == 0 &&
-         pthread_mutexattr_setrobust(&a, PTHREAD_MUTEX_ROBUST) == 0 && pthread_mutex_init(&b->ipc_lock, &a) == 0;
-    pthread_mutexattr_destroy(&a);
     b->magic = kBoardMagic;
     b->nranks = (uint32_t)nranks;
+  }
+  // this rank's socket for the descriptors of new allocations (named after the board: unique
+  // to the communicator)
+  if (ok) {
+    sock_base_ = std::string("mnccl") + (names.data() + 1);
+    sock_ = socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
+    sockaddr_un a;
+    unsigned len = 0;
+    sock_addr(rank, &a, &len);
+    if (sock_ < 0 || bind(sock_, (const sockaddr*)&a, (socklen_t)len) != 0) ok = 0;
   }
   std::vector<int> oks((size_t)nranks);
   boot.allgather(&ok, oks.data(), sizeof ok);  // also: rank 0's board is initialised
@@ -133,6 +159,8 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
   for (int v : oks) all = all && v;
   if (!all) {
     if (m != MAP_FAILED) munmap(m, board_bytes_);
+    if (sock_ >= 0) close(sock_);
+    sock_ = -1;
     if (rank == 0)
       fprintf(stderr, "[Mini-NCCL] warning: the ranks share no /dev/shm (per-call records): the read schedule is off "
               "and every call runs the ring\n");
@@ -141,13 +169,6 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
   board_ = static_cast<Board*>(m);
   boot.barrier();  // the board is initialised before anyone negotiates
 }
-
-void PeerBuffers::lock() {
-  const int e = pthread_mutex_lock(&board_->ipc_lock);
-  if (e == EOWNERDEAD) pthread_mutex_consistent(&board_->ipc_lock);  // its holder died: nothing to repair
-}
-
-void PeerBuffers::unlock() { pthread_mutex_unlock(&board_->ipc_lock); }
 
 void PeerBuffers::reap() {
   // allocations this process exported and has freed since my last call: my peers close their
@@ -160,22 +181,31 @@ void PeerBuffers::reap() {
 
 bool PeerBuffers::known(const void* p) const {
   uint64_t b = 0, i = 0;
-  hipIpcMemHandle_t h;
-  return !test_fake_ && ipc::find_live_export((uint64_t)(uintptr_t)p, &b, &i, &h);
+  ipc::Shared d;
+  return !test_fake_ && ipc::find_live_export((uint64_t)(uintptr_t)p, &b, &i, &d);
 }
 
 size_t PeerBuffers::mapped_allocations() const { return test_fake_ ? fake_maps_.size() : ipc::imports(); }
 
-// (base, id, handle) of the allocation holding p, exported once; false: it cannot be shared
-// (not a plain device allocation, or its address was exported before for another allocation)
-bool PeerBuffers::describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMemHandle_t* h) {
-  if (test_fake_) {  // CPU self-test: the pointer's page is its "allocation", the value its id
+// (base, id, export) of the allocation holding p, exported once; false: it cannot be shared
+// (not a plain device allocation, or its export failed)
+bool PeerBuffers::describe(const void* p, uint64_t* base, uint64_t* id, ipc::Shared* d) {
+  if (test_fake_) {  // CPU self-test: the pointer's page is its "allocation", the value its id,
+                     // a memfd its "dma-buf" (the descriptors really travel)
     *base = (uint64_t)(uintptr_t)p & ~(uint64_t)4095;
     *id = (uint64_t)(uintptr_t)p;
-    memset(h, 0, sizeof *h);
+    memset(d, 0, sizeof *d);
+    auto it = fake_fds_.find(std::make_pair(*base, *id));
+    if (it == fake_fds_.end())
+      it = fake_fds_.emplace(std::make_pair(*base, *id), memfd_create("mnccl-selftest", MFD_CLOEXEC)).first;
+    const int fd = it->second;
+    struct stat sb;
+    if (fd < 0 || fstat(fd, &sb) != 0) return false;
+    d->fd = fd;
+    d->ino = (uint64_t)sb.st_ino;
     return true;
   }
-  if (ipc::find_live_export((uint64_t)(uintptr_t)p, base, id, h)) return true;  // checked alive by reap()
+  if (ipc::find_live_export((uint64_t)(uintptr_t)p, base, id, d)) return true;  // checked alive by reap()
   // a new allocation (once per allocation): its range and id.  Not HIP_POINTER_ATTRIBUTE_RANGE_SIZE:
   // it comes back truncated to 32 bits (0 for a 4 GiB allocation on ROCm 7.2)
   hipDeviceptr_t b = 0;
@@ -188,35 +218,54 @@ bool PeerBuffers::describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMe
   }
   *base = (uint64_t)(uintptr_t)b;
   *id = bid;
-  return ipc::export_allocation(*base, bid, sz, h);
+  std::string why;
+  if (ipc::export_allocation(*base, bid, sz, d, &why)) return true;
+  if (!warned_export_) {
+    fprintf(stderr, "[Mini-NCCL] rank %d: a buffer cannot be shared with the peers (%s): its calls run the ring\n", rank_,
+            why.c_str());
+    warned_export_ = true;
+  }
+  return false;
 }
 
-// rank q's allocation (base, id) mapped here; nullptr (and *why) if it cannot be.  Caller holds
-// the board lock.
-char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h, std::string* why) {
+// rank q's allocation (base, id) mapped here; nullptr (and *why) if it cannot be.  fd: a
+// duplicate of the owner's descriptor if one arrived for it (-1 if none), always consumed.
+char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, int fd, const ipc::Shared& d, std::string* why) {
   if (test_fake_) {  // CPU self-test: no HIP; fail on the chosen call
+    struct stat sb;
+    const bool named = fd >= 0 && fstat(fd, &sb) == 0 && (uint64_t)sb.st_ino == d.ino;
+    if (fd >= 0) close(fd);
     for (const Known& k : fake_maps_)
       if (k.rank == q && k.base == base && k.id == id) return (char*)(uintptr_t)base;
     if (seq_ == test_fail_call_) {
       *why = "injected mapping failure (self-test)";
       return nullptr;
     }
+    if (!named) {
+      *why = fd < 0 ? "no descriptor arrived from the owner (self-test)"
+                    : "the received descriptor does not name the owner's (self-test)";
+      return nullptr;
+    }
     fake_maps_.push_back(Known{q, base, id});
     return (char*)(uintptr_t)base;
   }
   const uint64_t owner = nonces_[(size_t)q];
-  if (char* p = ipc::find_import(owner, base, id)) return p;
+  if (char* p = ipc::find_import(owner, base, id)) {
+    if (fd >= 0) close(fd);
+    return p;
+  }
   if (ipc::imports() >= kMaxImports) {
+    if (fd >= 0) close(fd);
     *why = "the process maps " + std::to_string(kMaxImports) + " peer allocations already";
     return nullptr;
   }
-  hipError_t e = hipSuccess;
-  char* p = ipc::open_import(owner, base, id, h, &e);
+  std::string w;
+  char* p = ipc::open_import(owner, base, id, fd, d, &w);
   if (!p) {
-    char msg[256];
-    snprintf(msg, sizeof msg, "hipIpcOpenMemHandle of rank %d's allocation (base 0x%llx, id %llu): %s", q,
-             (unsigned long long)base, (unsigned long long)id, hipGetErrorString(e));
-    *why = msg;
+    char msg[160];
+    snprintf(msg, sizeof msg, "import of rank %d's allocation (base 0x%llx, id %llu): ", q, (unsigned long long)base,
+             (unsigned long long)id);
+    *why = msg + w;
   }
   return p;
 }
@@ -227,8 +276,9 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
                                              const char** precv, bool* vec_all, const float* my_t, float* max_t) {
   const uint64_t k = ++seq_;
   const double t0 = now_s();
-  auto wait = [&](const std::atomic<uint64_t>& v, uint64_t want, int q, const char* what) {
-    for (int spins = 0; v.load(std::memory_order_acquire) < want; ++spins) {
+  // spins until ready() -- bounded by the peer q giving up and by the rendezvous limit
+  auto wait_for = [&](const std::function<bool()>& ready, int q, const char* what) {
+    for (int spins = 0; !ready(); ++spins) {
       if (board_->gave_up[q].v.load(std::memory_order_acquire) != 0)
         throw PeerGaveUp("read schedule: rank " + std::to_string(q) + " abandoned the communicator before all-reduce #" +
                          std::to_string(k));
@@ -240,7 +290,7 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
   };
   try {
     return negotiate_body(k, send, recv, eligible, count, dtype, op, sync_previous, psend, precv, vec_all, my_t, max_t,
-                          wait);
+                          wait_for);
   } catch (...) {
     // this rank gives up (a peer that never came or gave up itself): say so on the board, so
     // every peer waiting in a rendezvous with it fails at once instead of at its own limit (the
@@ -250,12 +300,123 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
   }
 }
 
-template <typename Wait>
+int PeerBuffers::try_send(int q, const FdMsg& m, const int* fds, int nfd) {
+  sockaddr_un a;
+  unsigned len = 0;
+  sock_addr(q, &a, &len);
+  iovec io{const_cast<FdMsg*>(&m), sizeof m};
+  char cbuf[CMSG_SPACE(2 * sizeof(int))];
+  memset(cbuf, 0, sizeof cbuf);
+  msghdr h;
+  memset(&h, 0, sizeof h);
+  h.msg_name = &a;
+  h.msg_namelen = (socklen_t)len;
+  h.msg_iov = &io;
+  h.msg_iovlen = 1;
+  if (nfd > 0) {
+    h.msg_control = cbuf;
+    h.msg_controllen = CMSG_SPACE((size_t)nfd * sizeof(int));
+    cmsghdr* c = CMSG_FIRSTHDR(&h);
+    c->cmsg_level = SOL_SOCKET;
+    c->cmsg_type = SCM_RIGHTS;
+    c->cmsg_len = CMSG_LEN((size_t)nfd * sizeof(int));
+    memcpy(CMSG_DATA(c), fds, (size_t)nfd * sizeof(int));
+  }
+  if (sendmsg(sock_, &h, MSG_DONTWAIT | MSG_NOSIGNAL) >= 0) return 1;
+  return errno == EAGAIN || errno == EWOULDBLOCK ? 0 : -1;
+}
+
+bool PeerBuffers::drain() {
+  bool any = false;
+  for (;;) {
+    FdMsg m;
+    memset(&m, 0, sizeof m);
+    iovec io{&m, sizeof m};
+    char cbuf[CMSG_SPACE(2 * sizeof(int))];
+    msghdr h;
+    memset(&h, 0, sizeof h);
+    h.msg_iov = &io;
+    h.msg_iovlen = 1;
+    h.msg_control = cbuf;
+    h.msg_controllen = sizeof cbuf;
+    const ssize_t r = recvmsg(sock_, &h, MSG_DONTWAIT | MSG_CMSG_CLOEXEC);
+    if (r < 0) return any;
+    any = true;
+    Pending p;
+    memset(&p, 0, sizeof p);
+    p.fd[0] = p.fd[1] = -1;
+    int nfd = 0;
+    for (cmsghdr* c = CMSG_FIRSTHDR(&h); c; c = CMSG_NXTHDR(&h, c))
+      if (c->cmsg_level == SOL_SOCKET && c->cmsg_type == SCM_RIGHTS) {
+        const int k = (int)((c->cmsg_len - CMSG_LEN(0)) / sizeof(int));
+        for (int i = 0; i < k; ++i) {
+          int f = -1;
+          memcpy(&f, CMSG_DATA(c) + (size_t)i * sizeof(int), sizeof f);
+          if (nfd < 2) p.fd[nfd++] = f;
+          else close(f);
+        }
+      }
+    if (r != (ssize_t)sizeof m || m.src < 0 || m.src >= nranks_ || m.nfd < 0 || m.nfd > 2) {
+      for (int i = 0; i < nfd; ++i) close(p.fd[i]);
+      continue;  // not ours
+    }
+    p.k = m.k;
+    p.src = m.src;
+    p.nfd = m.nfd < nfd ? m.nfd : nfd;  // a truncated message keeps only what arrived
+    for (int i = p.nfd; i < nfd; ++i) close(p.fd[i]), p.fd[i] = -1;
+    for (int i = 0; i < 2; ++i) p.base[i] = m.base[i], p.id[i] = m.id[i];
+    pending_.push_back(p);
+  }
+}
+
+void PeerBuffers::send_fds(int q, const FdMsg& m, const int* fds, const WaitFn& wait_for) {
+  int rc = 0;
+  // a peer's queue holds net.unix.max_dgram_qlen datagrams (10 by default) and every rank sends
+  // before it takes: a full queue is waited out while taking my own arrivals
+  wait_for([&] { return (rc = try_send(q, m, fds, m.nfd)) != 0 || (drain(), false); }, q, "take the descriptors of");
+  if (rc > 0) return;
+  // cannot pass the descriptors (e.g. the peer's descriptor table is full): the header alone, so
+  // the peer's mapping fails and the call runs the ring on every rank
+  FdMsg bare = m;
+  bare.nfd = 0;
+  wait_for([&] { return (rc = try_send(q, bare, nullptr, 0)) != 0 || (drain(), false); }, q, "take the descriptors of");
+  if (rc < 0) throw std::runtime_error(std::string("read schedule: sending to rank ") + std::to_string(q) + ": " +
+                                       strerror(errno));
+}
+
+PeerBuffers::Pending PeerBuffers::take_fds(int q, uint64_t k, const WaitFn& wait_for) {
+  Pending out;
+  memset(&out, 0, sizeof out);
+  out.fd[0] = out.fd[1] = -1;
+  bool found = false;
+  auto look = [&] {
+    for (size_t i = 0; i < pending_.size(); ++i) {
+      if (pending_[i].k < k) {  // an abandoned call's (cannot happen in a live communicator)
+        for (int j = 0; j < pending_[i].nfd; ++j) close(pending_[i].fd[j]);
+        pending_.erase(pending_.begin() + (long)i--);
+        continue;
+      }
+      if (pending_[i].src == q && pending_[i].k == k) {
+        out = pending_[i];
+        pending_.erase(pending_.begin() + (long)i);
+        return found = true;
+      }
+    }
+    return false;
+  };
+  wait_for([&] { return look() || (drain() && look()); }, q, "send the descriptors of");
+  return out;
+}
+
+template <typename WaitFor>
 PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible,
                                                   uint64_t count, int dtype, int op,
                                                   const std::function<void()>& sync_previous, const char** psend,
                                                   const char** precv, bool* vec_all, const float* my_t, float* max_t,
-                                                  const Wait& wait) {
+                                                  const WaitFor& wait_for) {
+  auto wait = [&](const std::atomic<uint64_t>& v, uint64_t want, int q, const char* what) {
+    wait_for([&] { return v.load(std::memory_order_acquire) >= want; }, q, what);
+  };
   const int slot = (int)(k % kBoardDepth);
   // my record slot is free once every peer has read the record kBoardDepth calls back
   if (k > (uint64_t)kBoardDepth)
@@ -266,7 +427,7 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
   BufDesc sd, rd;
   memset(&sd, 0, sizeof sd);
   memset(&rd, 0, sizeof rd);
-  bool ok = eligible && describe(send, &sd.base, &sd.id, &sd.h) && describe(recv, &rd.base, &rd.id, &rd.h);
+  bool ok = eligible && describe(send, &sd.base, &sd.id, &sd.d) && describe(recv, &rd.base, &rd.id, &rd.d);
   sd.raw = (uint64_t)(uintptr_t)send;
   rd.raw = (uint64_t)(uintptr_t)recv;
   sd.off = ok ? sd.raw - sd.base : 0;
@@ -344,9 +505,7 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
         sync_previous();
         synced = true;
       }
-      lock();
       closed_freed_ += ipc::close_import(nonces_[(size_t)q], fb, fi) ? 1 : 0;
-      unlock();
     }
 
   bool all = true, mismatch = false, aligned = true;
@@ -367,31 +526,68 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
   for (int q = 0; q < nranks_ && !need_agree; ++q)
     need_agree = !known_.count(Known{q, recs[(size_t)q].send.base, recs[(size_t)q].send.id}) ||
                  !known_.count(Known{q, recs[(size_t)q].recv.base, recs[(size_t)q].recv.id});
+  // The descriptors of the allocations new to this communicator travel first: every rank with a
+  // new buffer sends one datagram with them to every rank of another process, and every rank
+  // takes one from each such peer -- the same predicate on every rank, so nothing is left over.
+  auto is_new = [&](int q, const BufDesc& b) { return !known_.count(Known{q, b.base, b.id}); };
+  auto elsewhere = [&](int q) { return q != rank_ && nonces_[(size_t)q] != nonces_[(size_t)rank_]; };
+  std::vector<Pending> got((size_t)nranks_);
+  if (need_agree) {
+    FdMsg m;
+    memset(&m, 0, sizeof m);
+    m.k = k;
+    m.src = rank_;
+    int fds[2] = {-1, -1};
+    for (const BufDesc* b : {&recs[(size_t)rank_].send, &recs[(size_t)rank_].recv}) {
+      if (!is_new(rank_, *b) || (m.nfd == 1 && m.base[0] == b->base && m.id[0] == b->id)) continue;
+      m.base[m.nfd] = b->base;
+      m.id[m.nfd] = b->id;
+      fds[m.nfd++] = b->d.fd;
+    }
+    if (m.nfd)
+      for (int q = 0; q < nranks_; ++q)
+        if (elsewhere(q)) send_fds(q, m, fds, wait_for);
+    for (int q = 0; q < nranks_; ++q)
+      if (elsewhere(q) && (is_new(q, recs[(size_t)q].send) || is_new(q, recs[(size_t)q].recv)))
+        got[(size_t)q] = take_fds(q, k, wait_for);
+  }
+  // the descriptor that arrived for (q, base, id), handed over (-1: none)
+  auto fd_for = [&](int q, uint64_t base, uint64_t id) {
+    Pending& g = got[(size_t)q];
+    for (int i = 0; i < g.nfd; ++i)
+      if (g.base[i] == base && g.id[i] == id && g.fd[i] >= 0) {
+        const int f = g.fd[i];
+        g.fd[i] = -1;
+        return f;
+      }
+    return -1;
+  };
   bool mapped = true;
   std::string why;
-  bool locked = false;
-  for (int q = 0; q < nranks_ && mapped; ++q) {
+  for (int q = 0; q < nranks_; ++q) {
     const Seen& c = recs[(size_t)q];
-    if (q == rank_ || nonces_[(size_t)q] == nonces_[(size_t)rank_]) {
+    if (!elsewhere(q)) {
       psend[q] = (const char*)(uintptr_t)c.send.raw;  // this process's address space
       precv[q] = (const char*)(uintptr_t)c.recv.raw;
       continue;
     }
-    if (!locked && need_agree) {  // opens may happen: serialised with every process's opens / closes
-      lock();
-      locked = true;
-    }
-    const char* s = map_peer(q, c.send.base, c.send.id, c.send.h, &why);
-    const char* r = s ? map_peer(q, c.recv.base, c.recv.id, c.recv.h, &why) : nullptr;
+    const int fs = fd_for(q, c.send.base, c.send.id);
+    const int fr = fd_for(q, c.recv.base, c.recv.id);  // -1 too when send and recv share an allocation
+    const char* s = mapped ? map_peer(q, c.send.base, c.send.id, fs, c.send.d, &why) : nullptr;
+    const char* r = s ? map_peer(q, c.recv.base, c.recv.id, fr, c.recv.d, &why) : nullptr;
+    if (!s && fs >= 0 && !mapped) close(fs);  // map_peer consumes what it is given
+    if (!s && fr >= 0) close(fr);
     if (!s || !r) {
+      if (mapped) ++map_failures_;
       mapped = false;
-      ++map_failures_;
-      break;
+      continue;  // every descriptor that arrived is still consumed
     }
     psend[q] = s + c.send.off;
     precv[q] = r + c.recv.off;
   }
-  if (locked) unlock();
+  for (Pending& g : got)  // left over only after a failure
+    for (int i = 0; i < g.nfd; ++i)
+      if (g.fd[i] >= 0) close(g.fd[i]);
   if (!mapped && !need_agree)  // cannot happen (every buffer is mapped already); fail loudly if it does
     throw std::runtime_error("read schedule: a mapping of a known buffer is missing: " + why);
   Decision out = kRead;

@@ -4,15 +4,14 @@
 // so before each call every rank must know where its peers' buffers are mapped in its own
 // address space.  The reference exchanged IPC handles of the user buffers through rank 0 on
 // EVERY call over TCP and opened/closed them each time (RDMATransport.h:171-257).  Here:
-//  * each rank publishes a small record per call -- (allocation base, allocation id, offset, HIP
-//    IPC handle) of send and recv, count / dtype / op, whether it can take part, and which of
-//    its earlier exported allocations it has freed since -- on a board in host shared memory
-//    (one node: every rank is on this host), read by its peers with no network round trip;
-//  * a peer's allocation is opened once and kept open until its owner reports it freed (ipcreg.h:
-//    ROCm's IPC can map the wrong memory when an allocation is re-opened after a close, or a
-//    re-used address is exported again, so neither ever happens); opens and closes of all the
-//    communicator's processes are serialised by a lock on the board (an open racing another
-//    process's close can fail);
+//  * each rank publishes a small record per call -- (allocation base, allocation id, offset,
+//    dma-buf inode and offset) of send and recv, count / dtype / op, whether it can take part, and
+//    which of its earlier exported allocations it has freed since -- on a board in host shared
+//    memory (one node: every rank is on this host), read by its peers with no network round trip;
+//  * a call that brings an allocation new to the communicator carries its dma-buf descriptor to
+//    every peer process over a Unix datagram socket (SCM_RIGHTS); the peer maps it once and keeps
+//    the mapping until the owner reports the allocation freed (ipcreg.h: a dma-buf import keeps
+//    its memory alive and can never show another allocation, unlike round 2's hipIpc handles);
 //  * every rank reads the same records, so every rank takes the same decision: the read
 //    schedule when all ranks can, the communicator's scratch schedule otherwise, an error when
 //    the ranks disagree on count / dtype / op.
@@ -22,16 +21,19 @@
 
 #include <deque>
 #include <functional>
+#include <map>
 #include <stdexcept>
 #include <string>
 #include <unordered_set>
 #include <vector>
 
 #include "bootstrap.h"
+#include "ipcreg.h"
 
 namespace mnccl {
 
 struct Board;  // shared-memory layout (peerbuf.cpp)
+struct FdMsg;  // a datagram of descriptors (peerbuf.cpp)
 
 // A peer abandoned the communicator in an earlier rendezvous (its calls fail from now on).
 struct PeerGaveUp : std::runtime_error {
@@ -87,14 +89,25 @@ class PeerBuffers {
   void test_report_freed(uint64_t base, uint64_t id) { freed_.emplace_back(base, id); }
 
  private:
-  template <typename Wait>
+  // descriptors of new allocations, from one rank of another process, for call k
+  struct Pending {
+    uint64_t k;
+    int src, nfd;
+    uint64_t base[2], id[2];
+    int fd[2];
+  };
+  using WaitFn = std::function<void(const std::function<bool()>&, int, const char*)>;
+  template <typename WaitFor>
   Decision negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible, uint64_t count, int dtype,
                           int op, const std::function<void()>& sync_previous, const char** psend, const char** precv,
-                          bool* vec_all, const float* my_t, float* max_t, const Wait& wait);
-  bool describe(const void* p, uint64_t* base, uint64_t* id, hipIpcMemHandle_t* h);
-  char* map_peer(int q, uint64_t base, uint64_t id, const hipIpcMemHandle_t& h, std::string* why);
-  void lock();
-  void unlock();
+                          bool* vec_all, const float* my_t, float* max_t, const WaitFor& wait_for);
+  bool describe(const void* p, uint64_t* base, uint64_t* id, ipc::Shared* d);
+  char* map_peer(int q, uint64_t base, uint64_t id, int fd, const ipc::Shared& d, std::string* why);
+  void sock_addr(int q, void* addr, unsigned* len) const;
+  int try_send(int q, const FdMsg& m, const int* fds, int nfd);  // 1 sent, 0 queue full, -1 error
+  bool drain();  // takes every datagram waiting on my socket into pending_; true if any
+  void send_fds(int q, const FdMsg& m, const int* fds, const WaitFn& wait_for);
+  Pending take_fds(int q, uint64_t k, const WaitFn& wait_for);
 
   Board* board_ = nullptr;
   size_t board_bytes_ = 0;
@@ -121,6 +134,11 @@ class PeerBuffers {
   std::vector<Known> fake_maps_;   // CPU self-test: the "imports"
   uint64_t agreements_ = 0, map_failures_ = 0, closed_freed_ = 0;
   bool test_fake_ = false;
+  bool warned_export_ = false;
+  int sock_ = -1;          // this rank's datagram socket (abstract namespace), for descriptors
+  std::string sock_base_;  // the communicator's socket names: <base>-r<rank>
+  std::vector<Pending> pending_;  // arrived, not yet taken
+  std::map<std::pair<uint64_t, uint64_t>, int> fake_fds_;  // CPU self-test: a memfd per "allocation"
   uint64_t test_fail_call_ = 0;
 };
 

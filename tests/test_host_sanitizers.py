@@ -23,7 +23,7 @@ def test_host_logic_under_asan_ubsan(tmp_path):
         [os.path.join(CSRC, f) for f in ("sim.cpp", "bootstrap.cpp", "config.cpp", "peerbuf.cpp", "ipcreg.cpp")]
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
            "-fno-sanitize-recover=undefined", "-pthread", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
-           "-I" + CSRC, "-o", exe] + srcs + ["-L/opt/rocm/lib", "-lamdhip64", "-lrt", "-Wl,-rpath,/opt/rocm/lib"]
+           "-I" + CSRC, "-o", exe] + srcs + ["-L/opt/rocm/lib", "-lamdhip64", "-lhsa-runtime64", "-lrt", "-Wl,-rpath,/opt/rocm/lib"]
     subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300)
     env = dict(os.environ, SELFTEST_PORT=str(GW.free_port()), ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
                UBSAN_OPTIONS="print_stacktrace=1")
@@ -46,7 +46,7 @@ def _build_abi_selftest(tmp_path):
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
            "-fno-sanitize-recover=undefined", "-Wno-unused-result", "-pthread", "-D__HIP_PLATFORM_AMD__",
            "-I/opt/rocm/include", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-o", exe] + srcs + \
-        [obj, "-L/opt/rocm/lib", "-lamdhip64", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
+        [obj, "-L/opt/rocm/lib", "-lamdhip64", "-lhsa-runtime64", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
     subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=600)
     return exe
 
