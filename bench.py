@@ -177,7 +177,6 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
     """one communicator with `env` knobs; returns algbw GB/s (max time over ranks) and check"""
     tdt, ndt, esz = {"f32": (torch.float32, M.ncclFloat, 4), "bf16": (torch.bfloat16, M.ncclBfloat16, 2),
                      "f16": (torch.float16, M.ncclFloat16, 2)}[dtype]
-    env = dict(env, MINI_NCCL_TUNE=0)  # the point sets its schedule itself
     saved = {k: os.environ.get(k) for k in env}
     os.environ.update({k: str(v) for k, v in env.items()})
     comm = None

@@ -26,8 +26,9 @@
 extern "C" {
 #endif
 
-/* mncclVersion() of the library this header describes; mncclCommInfo_t grew in 300 */
-#define MNCCL_VERSION 300
+/* mncclVersion() of the library this header describes; mncclCommInfo_t grew in 300; 301:
+   user buffers shared as dma-bufs, MINI_NCCL_TUNE removed (same layout) */
+#define MNCCL_VERSION 301
 
 /* schedules; all produce bit-identical results (same fold order per element) */
 typedef enum {
@@ -61,9 +62,10 @@ typedef struct {
   int sys_fence;          /* MINI_NCCL_SYS_FENCE: system-scope release fence before each flag */
   double timeout_s;       /* MINI_NCCL_TIMEOUT_MS / 1000 */
   size_t scratch_bytes;   /* device scratch owned by this rank */
-  double tune_ms[2];      /* MINI_NCCL_TUNE=1 calibration at init (auto algo, 3+ ranks): ms per
-                             all-reduce of MINI_NCCL_TUNE_BYTES, ring / direct, max over
-                             ranks; 0 when not run (the default) */
+  double tune_ms[2];      /* always 0 since 301 (round 1's init-time ring / direct timing,
+                             MINI_NCCL_TUNE, was removed: MINI_NCCL_CALIBRATE measures read
+                             against the scratch schedule on real calls instead); kept for
+                             the layout */
   int pipelines;          /* channels x threads / 64 */
   int ranks_on_device;    /* ranks of this communicator on this rank's GPU (itself included) */
   size_t slot_bytes;      /* largest payload per message (MINI_NCCL_SLICE_SIZE unless the

@@ -164,8 +164,7 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
   info->sys_fence = k.sys_fence;
   info->timeout_s = k.timeout_ms / 1000.0;
   info->scratch_bytes = c->scratch_bytes();
-  info->tune_ms[0] = c->tune_ms(0);
-  info->tune_ms[1] = c->tune_ms(1);
+  info->tune_ms[0] = info->tune_ms[1] = 0.0;  // round 1's init-time calibration, removed in 0.3.1
   info->channels = c->workgroups();
   info->pipelines = c->wave_channels();
   info->ranks_on_device = c->ranks_on_device();
@@ -207,6 +206,6 @@ ncclResult_t mncclCommLinkProbe(ncclComm_t comm, int allPeers, size_t bytes, int
   }
 }
 
-int mncclVersion(void) { return MNCCL_VERSION; /* 0.3.0: mncclCommInfo_t grew, mncclCommGetInfoV */ }
+int mncclVersion(void) { return MNCCL_VERSION; /* 0.3.0: mncclCommInfo_t grew, mncclCommGetInfoV; 0.3.1: dma-buf sharing, no MINI_NCCL_TUNE */ }
 
 }  // extern "C"

@@ -98,8 +98,8 @@ struct PeerInfo {
   uint64_t host, nonce, pci;  // nonce: same process <=> same nonce; pci: the physical GPU
   uint64_t slice, scratch_bytes, mbox_bytes, scratch_cap;
   int32_t channels, slots, threads, abi;
-  int32_t window, signal_batch, algo, tune;
-  uint64_t min_slice, tune_bytes;
+  int32_t window, signal_batch, algo, pad1;
+  uint64_t min_slice;
   int32_t depth, overlap, pull, calibrate;
   uint64_t calibrate_bytes;
   hipIpcMemHandle_t scratch_h, mbox_h;
@@ -130,7 +130,6 @@ Comm::Comm(int nranks, int rank, const std::string& ip) : rank_(rank), nranks_(n
     setup_device_resources();
     boot_.connect(rank, nranks, ip, cfg_.port, cfg_.bootstrap_timeout_ms / 1000.0);
     exchange_and_map();
-    if (cfg_.algo < 0 && cfg_.tune && nranks >= 3) tune();
   } catch (...) {
     release();
     throw;
@@ -192,9 +191,7 @@ void Comm::exchange_and_map() {
   me.window = cfg_.window_size;
   me.signal_batch = cfg_.signal_batch;
   me.algo = cfg_.algo;
-  me.tune = cfg_.tune;
   me.min_slice = cfg_.min_slice;
-  me.tune_bytes = cfg_.tune_bytes;
   me.depth = cfg_.pipe_depth;
   me.overlap = cfg_.direct_overlap;
   me.pull = cfg_.pull;
@@ -218,11 +215,11 @@ void Comm::exchange_and_map() {
     if (p.slice != me.slice || p.channels != me.channels || p.slots != me.slots || p.threads != me.threads ||
         p.window != me.window || p.signal_batch != me.signal_batch || p.scratch_cap != me.scratch_cap ||
         p.min_slice != me.min_slice || p.depth != me.depth || p.overlap != me.overlap || p.pull != me.pull ||
-        p.algo != me.algo || p.tune != me.tune || p.tune_bytes != me.tune_bytes || p.abi != me.abi ||
+        p.algo != me.algo || p.abi != me.abi ||
         p.calibrate != me.calibrate || p.calibrate_bytes != me.calibrate_bytes)
       throw std::invalid_argument(
           "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SIGNAL_BATCH / SLOTS / CHANNELS / THREADS / SCRATCH_MB / MIN_SLICE / "
-          "PIPE_DEPTH / DIRECT_OVERLAP / PULL / ALGO / TUNE / TUNE_BYTES / CALIBRATE / CALIBRATE_BYTES differ between "
+          "PIPE_DEPTH / DIRECT_OVERLAP / PULL / ALGO / CALIBRATE / CALIBRATE_BYTES differ between "
           "ranks");
   }
   // the scratch schedule of MINI_NCCL_ALGO=auto / read (the read schedule's fallback for calls
@@ -300,56 +297,6 @@ void Comm::exchange_and_map() {
   std::vector<uint64_t> nonces((size_t)nranks_);
   for (int q = 0; q < nranks_; ++q) nonces[(size_t)q] = all[(size_t)q].nonce;
   pbuf_.init(boot_, rank_, nranks_, nonces, cfg_.port);
-}
-
-// MINI_NCCL_ALGO=auto with MINI_NCCL_TUNE=1 (opt-in; the default decides from the devices, see
-// exchange_and_map), from 3 ranks on: both schedules give the same bits.  Time one in-place
-// all-reduce of MINI_NCCL_TUNE_BYTES per rank with each (one warm-up, three timed), take the max
-// over ranks (allgather over the bootstrap, so every rank computes the same choice) and keep the
-// faster.
-void Comm::tune() {
-  const size_t count = cfg_.tune_bytes / 4;
-  float* buf = nullptr;
-  hipStream_t st = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  double ms[2] = {0.0, 0.0};
-  bool ok = true;
-  try {
-    hip_check(hipMalloc((void**)&buf, count * 4), "tune alloc");
-    hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "tune stream");
-    hip_check(hipMemsetAsync(buf, 0, count * 4, st), "tune memset");
-    hip_check(hipStreamSynchronize(st), "tune sync");
-    hip_check(hipEventCreate(&e0), "tune event");
-    hip_check(hipEventCreate(&e1), "tune event");
-    for (int a = 0; a < 2 && ok; ++a) {
-      algo_ = a;
-      ok = allreduce(buf, buf, count, kF32, kSum, st) == ncclSuccess;
-      hip_check(hipStreamSynchronize(st), "tune sync");
-      boot_.barrier();
-      hip_check(hipEventRecord(e0, st), "tune event");
-      for (int i = 0; i < 3 && ok; ++i) ok = allreduce(buf, buf, count, kF32, kSum, st) == ncclSuccess;
-      hip_check(hipEventRecord(e1, st), "tune event");
-      hip_check(hipEventSynchronize(e1), "tune wait");
-      float t = 0.f;
-      hip_check(hipEventElapsedTime(&t, e0, e1), "tune time");
-      ms[a] = t / 3.0;
-    }
-  } catch (...) {
-    ok = false;
-  }
-  if (e0) hipEventDestroy(e0);
-  if (e1) hipEventDestroy(e1);
-  if (st) hipStreamDestroy(st);
-  if (buf) hipFree(buf);
-  if (!ok || sticky_ != ncclSuccess) throw std::runtime_error("auto-tune all-reduce failed");
-  std::vector<double> all((size_t)nranks_ * 2);
-  boot_.allgather(ms, all.data(), sizeof ms);
-  for (int q = 0; q < nranks_; ++q)
-    for (int a = 0; a < 2; ++a) tune_ms_[a] = std::max(tune_ms_[a], all[(size_t)q * 2 + a]);
-  algo_ = tune_ms_[1] <= tune_ms_[0] ? 1 : 0;
-  if (cfg_.debug && rank_ == 0)
-    fprintf(stderr, "[Mini-NCCL] auto-tune %zu B: ring %.3f ms, direct %.3f ms -> %s\n", count * 4, tune_ms_[0],
-            tune_ms_[1], algo_ ? "direct" : "ring");
 }
 
 Comm::~Comm() {

@@ -45,7 +45,6 @@ class Comm {
   const PeerBuffers& peer_buffers() const { return pbuf_; }
   int scratch_algo() const { return scratch_algo_; }
   // calibration of MINI_NCCL_ALGO=auto with MINI_NCCL_TUNE=1 (max over ranks, ms per call; 0 = not run)
-  double tune_ms(int a) const { return tune_ms_[a & 1]; }
   // rank processes / communicators whose GPU is this rank's GPU (this rank included)
   int ranks_on_device() const { return ranks_on_device_; }
   ncclResult_t async_error();
@@ -64,7 +63,6 @@ class Comm {
   void setup_device_resources();
   void release();
   void exchange_and_map();
-  void tune();
   ncclResult_t wait_for(hipStream_t stream, uint32_t seq);
   enum class Reach { kDevice, kMapped, kStaged };
   Reach reach(const void* p, const void** kernel_ptr, bool* local) const;
@@ -100,7 +98,6 @@ class Comm {
   bool calib_rec_[2] = {false, false};
   int ranks_on_device_ = 1;
   uint32_t call_seq_ = 0;        // kernel launches of this communicator (the kernel's start word)
-  double tune_ms_[2] = {0.0, 0.0};
   Bootstrap boot_;
 
   char* scratch_ = nullptr;      // uncached device memory, peers write into it

@@ -72,10 +72,6 @@ Config Config::from_env() {
   if (c.pipe_depth < 1) c.pipe_depth = 1;
   c.direct_overlap = env_int("MINI_NCCL_DIRECT_OVERLAP", 1) != 0;
   c.pull = env_int("MINI_NCCL_PULL", 0) != 0;
-  c.tune = env_int("MINI_NCCL_TUNE", 0) != 0;
-  long long tb = env_int("MINI_NCCL_TUNE_BYTES", 64LL << 20);
-  if (tb < (1LL << 20)) tb = 1LL << 20;
-  c.tune_bytes = (size_t)(tb & ~255LL);
   c.stage_host = env_int("MINI_NCCL_STAGE_HOST", 0) != 0;
   if (const char* cal = std::getenv("MINI_NCCL_CALIBRATE"); cal && *cal)
     c.calibrate = strcmp(cal, "auto") == 0 ? -1 : env_int("MINI_NCCL_CALIBRATE", 0) != 0 ? 1 : 0;
@@ -93,11 +89,11 @@ std::string Config::describe() const {
   char b[384];
   snprintf(b, sizeof b,
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, scratch_cap=%zu MiB, algo=%s, "
-           "blocking=%d, sys_fence=%d, min_slice=%zu, depth=%d, pull=%d, tune=%d, stage_host=%d, calibrate=%d (%zu B), "
+           "blocking=%d, sys_fence=%d, min_slice=%zu, depth=%d, pull=%d, stage_host=%d, calibrate=%d (%zu B), "
            "timeout=%.0f ms, port=%d",
            slice_size, window_size, signal_batch, slots, channels, threads, scratch_cap >> 20,
            algo < 0 ? "auto" : algo == 2 ? "read" : algo ? "direct" : "ring", blocking,
-           sys_fence, min_slice, pipe_depth, pull, tune, stage_host, calibrate, calibrate_bytes, timeout_ms, port);
+           sys_fence, min_slice, pipe_depth, pull, stage_host, calibrate, calibrate_bytes, timeout_ms, port);
   return b;
 }
 

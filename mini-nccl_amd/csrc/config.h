@@ -24,8 +24,6 @@ struct Config {
   int pipe_depth = 1;              // MINI_NCCL_PIPE_DEPTH slices per pipeline targeted for small calls
   int direct_overlap = 1;          // MINI_NCCL_DIRECT_OVERLAP next iteration's raw pushes before this one's results
   int pull = 0;                    // MINI_NCCL_PULL   1: slots in the sender's scratch, loaded over the link
-  int tune = 0;                    // MINI_NCCL_TUNE   1: auto algo times both schedules at init (n >= 3)
-  size_t tune_bytes = 64u << 20;   // MINI_NCCL_TUNE_BYTES per-rank buffer of that calibration
   int stage_host = 0;              // MINI_NCCL_STAGE_HOST pinned host buffers: 0 = kernel maps them, 1 = staged copy
   int calibrate = 0;               // MINI_NCCL_CALIBRATE auto algo: time read vs the scratch schedule on the first
                                    //   large calls and keep the faster; 0 off (default: the scratch schedule has not

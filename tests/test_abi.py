@@ -140,7 +140,7 @@ def test_config_from_env(sim_lib, monkeypatch):
     # (channels=0, schedule.h pipeline_geometry); no auto-tune at init; 512 MiB scratch cap
     assert "SLICE_SIZE=131072 B" in s and "WINDOW=64" in s and "BATCH=16" in s and "channels=0" in s
     assert "algo=auto" in s and "threads=64" in s and "sys_fence=0" in s and "min_slice=1024" in s
-    assert "tune=0" in s and "scratch_cap=512 MiB" in s
+    assert "scratch_cap=512 MiB" in s
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", "0")       # Config.h:50: 0 -> 1024
     monkeypatch.setenv("MINI_NCCL_WINDOW_SIZE", "-3")     # Config.h:51: <= 0 -> 1
     monkeypatch.setenv("MINI_NCCL_SLOTS", "1")            # clamped to 2 (deadlock-free minimum)

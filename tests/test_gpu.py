@@ -57,7 +57,7 @@ class TestLocalReduce:
 def _run_allreduce(n, cases, env=None, timeout=300, barrier=True):
     port = GW.free_port()
     # every case sets its schedule explicitly; the ranks line up before each call (barrier)
-    e = {"MINI_NCCL_TIMEOUT_MS": "30000", "MINI_NCCL_TUNE": "0"}
+    e = {"MINI_NCCL_TIMEOUT_MS": "30000"}
     e.update(env or {})
     out = GW.run_ranks(GW.allreduce_rank, n, lambda r: (r, n, port, cases, e), timeout,
                        barrier=barrier)
@@ -135,7 +135,7 @@ def test_skewed_ranks_varying_data(dev, algo, blocking):
 def test_auto_schedule_from_devices_no_init_allreduce(dev):
     # MINI_NCCL_ALGO=auto (default): the read schedule, with a scratch fallback that comes from
     # the gathered device records (every rank on one GPU -> ring at any n); no all-reduce runs
-    # at init (tune_ms stays 0)
+    # at init
     port = GW.free_port()
     out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {}), 120)
     assert all("error" not in out[r] for r in range(3)), out
@@ -149,19 +149,6 @@ def test_auto_schedule_from_devices_no_init_allreduce(dev):
     port = GW.free_port()
     out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {"MINI_NCCL_ALGO": "direct"}), 120)
     assert out[0]["info"]["tune_ms"] == [0.0, 0.0] and out[0]["info"]["algo"] == 1
-
-
-def test_auto_tune_opt_in_picks_the_faster_schedule(dev):
-    # MINI_NCCL_TUNE=1: both schedules timed at init (max over ranks, every rank sees the same
-    # numbers), the faster kept
-    port = GW.free_port()
-    env = {"MINI_NCCL_TUNE": "1", "MINI_NCCL_TUNE_BYTES": str(8 << 20)}
-    out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, env), 120)
-    assert all("error" not in out[r] for r in range(3)), out
-    infos = [out[r]["info"] for r in range(3)]
-    t = infos[0]["tune_ms"]
-    assert t[0] > 0 and t[1] > 0 and all(i["tune_ms"] == t for i in infos)
-    assert all(i["algo"] == (1 if t[1] <= t[0] else 0) for i in infos)
 
 
 def test_measured_choice_between_read_and_scratch(dev):
@@ -334,7 +321,7 @@ def test_allreduce_8_ranks_full_size(dev, dtype, algos, gib, knobs):
     exp = GW.block_digests(O.ring_fold_parallel(xs, dtype, "sum"))
     del xs
     port = GW.free_port()
-    env = {"MINI_NCCL_TIMEOUT_MS": "60000", "MINI_NCCL_TUNE": "0", "GPU_MAX_HW_QUEUES": "2", **knobs}
+    env = {"MINI_NCCL_TIMEOUT_MS": "60000", "GPU_MAX_HW_QUEUES": "2", **knobs}
     out = GW.run_ranks(GW.fullsize_rank, n, lambda r: (r, n, port, env, dtype, count, algos), 600, barrier=True)
     assert sorted(out) == list(range(n)), f"only ranks {sorted(out)} reported"
     for r in range(n):
@@ -377,7 +364,7 @@ def test_allreduce_async_mode(dev):
 @pytest.mark.parametrize("algo", ["ring", "direct", "read"])
 def test_destroy_waits_for_calls_in_flight(dev, algo):
     port = GW.free_port()
-    env = {"MINI_NCCL_BLOCKING": "0", "MINI_NCCL_ALGO": algo, "MINI_NCCL_TUNE": "0", "MINI_NCCL_TIMEOUT_MS": "30000"}
+    env = {"MINI_NCCL_BLOCKING": "0", "MINI_NCCL_ALGO": algo, "MINI_NCCL_TIMEOUT_MS": "30000"}
     out = GW.run_ranks(GW.destroy_inflight_rank, 3, lambda r: (r, 3, port, env), 180)
     assert sorted(out) == [0, 1, 2], out
     for r in range(3):
@@ -438,7 +425,7 @@ def test_allreduce_hip_graph_capture_and_replay(dev, algo):
 @pytest.mark.parametrize("algo", ["ring", "direct", "read"])
 def test_calls_on_alternating_streams_are_ordered(dev, algo):
     port = GW.free_port()
-    env = {"MINI_NCCL_TIMEOUT_MS": "20000", "MINI_NCCL_ALGO": algo, "MINI_NCCL_BLOCKING": "0", "MINI_NCCL_TUNE": "0"}
+    env = {"MINI_NCCL_TIMEOUT_MS": "20000", "MINI_NCCL_ALGO": algo, "MINI_NCCL_BLOCKING": "0"}
     out = GW.run_ranks(GW.streams_rank, 3, lambda r: (r, 3, port, env, 6), 180)
     assert sorted(out) == [0, 1, 2], out
     for r in range(3):
@@ -466,7 +453,7 @@ def test_single_rank_is_copy_only(dev):
 
 
 @pytest.mark.parametrize("knob,values", [("MINI_NCCL_SLICE_SIZE", ("131072", "65536")), ("MINI_NCCL_PULL", ("0", "1")),
-                                         ("MINI_NCCL_ALGO", ("ring", "direct")), ("MINI_NCCL_TUNE", ("0", "1")),
+                                         ("MINI_NCCL_ALGO", ("ring", "direct")), ("MINI_NCCL_CALIBRATE", ("0", "1")),
                                          ("MINI_NCCL_WINDOW_SIZE", ("64", "16"))])
 def test_mismatched_config_is_system_error(dev, knob, values):
     # every init failure is ncclSystemError, as in the reference (api.cpp:62-65)

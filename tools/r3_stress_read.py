@@ -29,7 +29,7 @@ def main():
         cases.append(dict(dtype=("f32", "bf16", "f16")[i % 3], op="sum", count=max(count, a.ranks), inplace=bool(i % 4 == 0),
                           algo=2, calls=1, seed=5000 + i, special=False, offset=0, fresh=bool(i % 3 == 1)))
     port = GW.free_port()
-    env = {"MINI_NCCL_TIMEOUT_MS": "30000", "MINI_NCCL_TUNE": "0", "GPU_MAX_HW_QUEUES": "2"}
+    env = {"MINI_NCCL_TIMEOUT_MS": "30000", "GPU_MAX_HW_QUEUES": "2"}
     out = GW.run_ranks(GW.allreduce_rank, a.ranks, lambda r: (r, a.ranks, port, cases, env), 1800, barrier=True)
     ok = len(out) == a.ranks
     for r in sorted(out):
