@@ -150,7 +150,10 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
     sockaddr_un a;
     unsigned len = 0;
     sock_addr(rank, &a, &len);
-    if (sock_ < 0 || bind(sock_, (const sockaddr*)&a, (socklen_t)len) != 0) ok = 0;
+    const int one = 1;  // the sender's credentials come with every datagram (checked in drain)
+    if (sock_ < 0 || bind(sock_, (const sockaddr*)&a, (socklen_t)len) != 0 ||
+        setsockopt(sock_, SOL_SOCKET, SO_PASSCRED, &one, sizeof one) != 0)
+      ok = 0;
   }
   std::vector<int> oks((size_t)nranks);
   boot.allgather(&ok, oks.data(), sizeof ok);  // also: rank 0's board is initialised
@@ -332,7 +335,7 @@ bool PeerBuffers::drain() {
     FdMsg m;
     memset(&m, 0, sizeof m);
     iovec io{&m, sizeof m};
-    char cbuf[CMSG_SPACE(2 * sizeof(int))];
+    alignas(cmsghdr) char cbuf[CMSG_SPACE(2 * sizeof(int)) + CMSG_SPACE(sizeof(ucred))];
     msghdr h;
     memset(&h, 0, sizeof h);
     h.msg_iov = &io;
@@ -346,7 +349,13 @@ bool PeerBuffers::drain() {
     memset(&p, 0, sizeof p);
     p.fd[0] = p.fd[1] = -1;
     int nfd = 0;
-    for (cmsghdr* c = CMSG_FIRSTHDR(&h); c; c = CMSG_NXTHDR(&h, c))
+    bool mine = false;  // sent by a process of this user (abstract sockets carry no permissions)
+    for (cmsghdr* c = CMSG_FIRSTHDR(&h); c; c = CMSG_NXTHDR(&h, c)) {
+      if (c->cmsg_level == SOL_SOCKET && c->cmsg_type == SCM_CREDENTIALS) {
+        ucred u;
+        memcpy(&u, CMSG_DATA(c), sizeof u);
+        mine = u.uid == getuid();
+      }
       if (c->cmsg_level == SOL_SOCKET && c->cmsg_type == SCM_RIGHTS) {
         const int k = (int)((c->cmsg_len - CMSG_LEN(0)) / sizeof(int));
         for (int i = 0; i < k; ++i) {
@@ -356,7 +365,8 @@ bool PeerBuffers::drain() {
           else close(f);
         }
       }
-    if (r != (ssize_t)sizeof m || m.src < 0 || m.src >= nranks_ || m.nfd < 0 || m.nfd > 2) {
+    }
+    if (!mine || r != (ssize_t)sizeof m || m.src < 0 || m.src >= nranks_ || m.nfd < 0 || m.nfd > 2) {
       for (int i = 0; i < nfd; ++i) close(p.fd[i]);
       continue;  // not ours
     }
