@@ -79,9 +79,15 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
                 m = case.get(key, dflt)
                 return m[rank % len(m)] if isinstance(m, (list, tuple)) else m
             fresh = case.get("fresh", False)  # own hipMalloc / hipFree (allocation churn), not the cache
-            send = hip_rt.buffer(placement("mem", "device"), nbytes + off, fresh)
-            recv = send if inplace else hip_rt.buffer(placement("recv_mem", placement("mem", "device")), nbytes + off,
-                                                      fresh)
+            if case.get("one_alloc") and not inplace:
+                # send and recv as two regions of ONE device allocation (one export serves both)
+                whole = hip_rt.buffer("device", 2 * (nbytes + off) + 256, fresh)
+                send = hip_rt.View(whole, 0, nbytes + off)
+                recv = hip_rt.View(whole, (nbytes + off + 255) // 256 * 256, nbytes + off)
+            else:
+                send = hip_rt.buffer(placement("mem", "device"), nbytes + off, fresh)
+                recv = send if inplace else hip_rt.buffer(placement("recv_mem", placement("mem", "device")),
+                                                          nbytes + off, fresh)
             if not inplace:
                 recv.fill_byte(0xAB)
             rc = 0
@@ -132,6 +138,54 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
         info = comm.info()
         rc = comm.destroy()
         out_q.put((rank, {"results": results, "destroy": rc, "info": info}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
+def two_comms_rank(rank, n, ports, env, rounds, out_q):
+    """Two communicators in one process sharing the same send / recv buffers, calls alternating
+    between them; every other round on fresh allocations (freed after it).  Each communicator
+    brings the buffers as new the first time (the owner sends their dma-bufs again, the peer's
+    import is found and the duplicate closed); frees reach both through the process's freed log."""
+    try:
+        os.environ.update(env)
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        hip_rt.set_device(0)
+        comms = []
+        for p in ports:
+            os.environ["MINI_NCCL_PORT"] = str(p)
+            comms.append(M.Comm(n, rank, "127.0.0.1"))
+        for c in comms:
+            c.set_algo(2)
+        stream = hip_rt.Stream()
+        code, npd = O.DTYPES["f32"]
+        bad, rcs, algos = 0, [], []
+        for i in range(rounds):
+            count = 70001 + 3 * i
+            fresh = i % 2 == 1
+            send = hip_rt.buffer("device", count * 4, fresh)
+            recv = hip_rt.buffer("device", count * 4, fresh)
+            for j, c in enumerate(comms + comms):
+                xs = make_inputs(n, count, "f32", 700 + 10 * i + j, False)
+                exp = O.allreduce(xs, "f32", "sum")[rank]
+                send.upload(xs[rank])
+                rc = c.all_reduce(send.ptr, recv.ptr, count, code, O.OPS["sum"], stream.handle)
+                stream.sync()
+                rcs.append(rc)
+                got = recv.download(npd, count)
+                bad += compare(got, exp, "f32", True)[0]
+                algos.append(c.info()["last_algo"])
+            send.free()
+            recv.free()
+        infos = [c.info() for c in comms]
+        stream.destroy()
+        destroy = [c.destroy() for c in comms]
+        out_q.put((rank, {"bad": bad, "rcs": rcs, "algos": algos, "destroy": destroy,
+                          "ipc_open_failures": infos[0]["ipc_open_failures"],
+                          "read_map_failures": [x["read_map_failures"] for x in infos],
+                          "closed_freed": [x["closed_freed"] for x in infos]}))
     except Exception:
         out_q.put((rank, {"error": traceback.format_exc()}))
 

@@ -122,6 +122,29 @@ class DeviceBuffer:
             self.ptr = 0
 
 
+class View:
+    """A region of another buffer (its owner is freed with the view at offset 0)."""
+
+    def __init__(self, owner, offset, nbytes):
+        self.owner, self.offset, self.nbytes = owner, offset, nbytes
+        self.ptr = owner.ptr + offset
+
+    def upload(self, arr, offset=0):
+        self.owner.upload(arr, self.offset + offset)
+
+    def download(self, dtype, count, offset=0):
+        return self.owner.download(dtype, count, self.offset + offset)
+
+    def fill_byte(self, value):
+        check(lib().hipMemset(self.ptr, value, self.nbytes), "hipMemset")
+        check(lib().hipDeviceSynchronize(), "hipDeviceSynchronize")
+
+    def free(self):
+        if self.offset == 0:
+            self.owner.free()
+        self.ptr = 0
+
+
 class HostBuffer:
     """Pinned host memory (hipHostMalloc, the reference perf_test's cudaHostAlloc buffers,
     tests/perf_test.cpp:78-79): the all-reduce kernel addresses it through its device mapping."""

@@ -276,6 +276,35 @@ def test_read_schedule_allocation_churn(dev):
         assert all(x["live_exports"] <= 2 for x in res)
 
 
+def test_read_schedule_send_recv_in_one_allocation(dev):
+    # out of place with send and recv two regions of ONE allocation on every rank: the owner's
+    # descriptor datagram carries that allocation once, both mappings come from one import;
+    # cached and fresh allocations, every call run by the read schedule and bit-exact
+    n = 3
+    cases = [_case(count=300007 + 5 * i, algo=2, seed=1500 + i, one_alloc=True, fresh=(i % 2 == 1), calls=2, vary=True)
+             for i in range(6)]
+    out = _run_allreduce(n, cases, timeout=300)
+    for r in range(n):
+        assert all(x["last_algo"] == 2 for x in out[r]["results"])
+
+
+def test_read_schedule_two_communicators_share_buffers(dev):
+    # two communicators per rank process over the same ranks, the same buffers used on both
+    # (calls alternate); every other round on fresh allocations that are then freed -- every call
+    # read and bit-exact, no import fails, frees reach both communicators
+    n = 3
+    ports = (GW.free_port(), GW.free_port())
+    out = GW.run_ranks(GW.two_comms_rank, n, lambda r: (r, n, ports, {"MINI_NCCL_TIMEOUT_MS": "30000"}, 6), 300)
+    assert sorted(out) == list(range(n)), out
+    for r in range(n):
+        o = out[r]
+        assert "error" not in o, o["error"]
+        assert o["bad"] == 0 and all(rc == 0 for rc in o["rcs"]) and o["destroy"] == [0, 0], o
+        assert all(a == 2 for a in o["algos"]), o["algos"]
+        assert o["ipc_open_failures"] == 0 and o["read_map_failures"] == [0, 0], o
+        assert sum(o["closed_freed"]) >= 2 * (n - 1) * 2, o  # rounds 1 and 3's fresh buffers at least
+
+
 def test_read_schedule_frees_mapped_allocations(dev):
     # large allocations (64-96 MiB) mapped by every peer and then freed by their owner while the
     # peers still hold the mappings (hipFree before the importers close: the owner reports the
