@@ -467,7 +467,8 @@ void Comm::wait_previous_call() {
 }
 
 void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
-                  uint32_t seq, bool vec, const char* const* psend, const char* const* precv) {
+                  uint32_t seq, bool vec, const char* const* psend, const char* const* precv,
+                  size_t tail_bytes) {
   const int n = nranks_;
   CollParams p;
   memset(&p, 0, sizeof p);
@@ -505,6 +506,7 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.sys_fence = cfg_.sys_fence;
   p.direct_overlap = cfg_.direct_overlap;
   p.pull = cfg_.pull;
+  p.tail_bytes = tail_bytes;
   const int nt = cfg_.threads, wg = algo == 2 ? A / geo_.waves : geo_.workgroups;
   hipError_t e = algo == 2   ? launch_read(dtype, op, vec, wg, nt, p, stream)
                  : algo == 1 ? launch_direct(dtype, op, vec, wg, nt, p, stream)
@@ -579,13 +581,10 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
       if (rr == Reach::kStaged) krecv = stage_;  // also in place when send is staged too
     }
     // elements past n*chunk keep this rank's own input (the reference copies the whole
-    // buffer and never touches the tail, api.cpp:173-175 + mini_nccl.cu:69); the ring
-    // writes every other element of recv, so only the tail needs the copy
+    // buffer and never touches the tail, api.cpp:173-175 + mini_nccl.cu:69); the kernels
+    // write every other element of recv and copy the tail themselves (kernels.hip copy_tail)
     const size_t body = chunk_bytes * (size_t)n;
-    if (ksend != krecv && bytes > body)
-      hip_check(hipMemcpyAsync((char*)krecv + body, (const char*)ksend + body, bytes - body, hipMemcpyDefault,
-                               stream),
-                "tail copy");
+    const size_t tail = ksend != krecv && bytes > body ? bytes - body : 0;
     // 16-byte vector path whenever every message's local base is dword-aligned (vectors may
     // straddle 16-byte boundaries on the local side; each message's last len % 16 bytes go
     // element by element); element-wise path otherwise (2-byte types with odd chunks)
@@ -661,7 +660,7 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
         if (!e) hip_check(hipEventCreate(&e), "calibration event");
       hip_check(hipEventRecord(calib_ev_[measure][0], stream), "calibration event");
     }
-    launch(algo, ksend, krecv, chunk_bytes, dtype, op, stream, seq, vec, psend, precv);
+    launch(algo, ksend, krecv, chunk_bytes, dtype, op, stream, seq, vec, psend, precv, tail);
     if (measure >= 0) {
       hip_check(hipEventRecord(calib_ev_[measure][1], stream), "calibration event");
       calib_rec_[measure] = true;

@@ -69,7 +69,8 @@ class Comm {
   void ensure_stage(size_t bytes, hipStream_t stream);
   // algo: 0 ring, 1 direct, 2 read (psend / precv: every rank's buffers mapped here)
   void launch(int algo, const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
-              uint32_t seq, bool vec, const char* const* psend = nullptr, const char* const* precv = nullptr);
+              uint32_t seq, bool vec, const char* const* psend = nullptr, const char* const* precv = nullptr,
+              size_t tail_bytes = 0);
   void wait_previous_call();
   ncclResult_t check_status();
   // MINI_NCCL_CALIBRATE: read the timings of this rank's measured calls whose events completed

@@ -37,6 +37,8 @@ struct CollParams {
                            // kernel's grid may run fewer (schedule.h read_pipelines)
   const char* peer_send[16];  // read schedule: every rank's send buffer, mapped here (own at [rank])
   const char* peer_recv[16];  // read schedule: every rank's recv buffer, mapped here
+  uint64_t tail_bytes;        // bytes past n * chunk_bytes that the kernel copies send -> recv
+                              // (the reference leaves them as its copy made them, api.cpp:173-175)
 };
 
 constexpr int kMaxRanks = 16;

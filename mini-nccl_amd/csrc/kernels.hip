@@ -355,6 +355,18 @@ __device__ __forceinline__ void signal_start(const CollParams& p) {
   if (blockIdx.x == 0 && threadIdx.x == 0) st_sys32(p.started, p.call_seq);
 }
 
+// The count % n elements past the chunks keep this rank's own input (api.cpp:173-175 copies the
+// whole buffer, mini_nccl.cu:69 never touches the tail): pipeline 0 copies them, byte by byte
+// (under 128 bytes), so a call is one launch.  Measured on the one-GPU box: a copy kernel queued
+// in front of a persistent kernel can find no room left by the co-located ranks' persistent
+// kernels, which then wait for this rank's forever (tools/dr_probe.py,
+// profiles/r3_device_rendezvous.txt: 2 of 2 runs stalled with the copy, 4 of 4 clean without).
+__device__ __forceinline__ void copy_tail(const CollParams& p, int w, int lane) {
+  if (w != 0 || p.tail_bytes == 0) return;
+  const uint64_t off = p.chunk_bytes * (uint64_t)p.n;
+  for (uint64_t i = (uint64_t)lane; i < p.tail_bytes; i += 64) p.recv[off + i] = p.send[off + i];
+}
+
 // channel geometry: one channel per wave
 struct WaveId {
   int lane, wv, w, C;
@@ -384,6 +396,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) ring_kernel(Col
   const WaveId id = wave_id();
   const int lane = id.lane, w = id.w, C = id.C;
   const int n = p.n, r = p.rank, K = p.nslots;
+  copy_tail(p, w, lane);
   const int prev = mod_n(r - 1, n), next = mod_n(r + 1, n);
   const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox};
   // per-pair message counters: the FIFO to `next` and the FIFO from `prev` on this channel
@@ -578,6 +591,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) direct_kernel(C
   const WaveId id = wave_id();
   const int lane = id.lane, w = id.w, C = id.C, wv = id.wv;
   const int n = p.n, r = p.rank, K = p.nslots;
+  copy_tail(p, w, lane);
   // per-wave rows: per-pair FIFO counters at call start, and this iteration's positions
   __shared__ u64 s_tx[kMaxWaves][kMaxRanks], s_rx[kMaxWaves][kMaxRanks];
   __shared__ u64 s_rx0[kMaxWaves][kMaxRanks], s_tx1[kMaxWaves][kMaxRanks];
@@ -929,6 +943,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
   // (its grid), slice s on pipeline s mod A
   const int lane = id.lane, w = id.w, C = p.pipes, A = id.C, wv = id.wv;
   const int n = p.n, r = p.rank;
+  copy_tail(p, w, lane);
   __shared__ u64 s_tx[kMaxWaves][kMaxRanks], s_rx[kMaxWaves][kMaxRanks];
   u64* tx = s_tx[wv];
   u64* rx = s_rx[wv];
