@@ -615,8 +615,13 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
       if (!c.map_ok && failed < 0) failed = q;
     }
     if (failed >= 0) {
-      fprintf(stderr, "[Mini-NCCL] rank %d: all-reduce #%llu falls back to the scratch schedule: rank %d could not map "
-              "a peer's buffer%s%s\n", rank_, (unsigned long long)k, failed, why.empty() ? "" : ": ", why.c_str());
+      // a driver that cannot import the peers' memory fails every call alike: say so at the 1st,
+      // 2nd, 4th, 8th ... fallback, not at every call
+      ++fallbacks_;
+      if ((fallbacks_ & (fallbacks_ - 1)) == 0)
+        fprintf(stderr, "[Mini-NCCL] rank %d: all-reduce #%llu falls back to the scratch schedule (fallback %llu): rank "
+                "%d could not map a peer's buffer%s%s\n", rank_, (unsigned long long)k,
+                (unsigned long long)fallbacks_, failed, why.empty() ? "" : ": ", why.c_str());
       out = kFallback;
     }
   }

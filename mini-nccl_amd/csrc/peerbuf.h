@@ -133,6 +133,7 @@ class PeerBuffers {
   std::deque<Known> known_order_;  // insertion order, to bound known_
   std::vector<Known> fake_maps_;   // CPU self-test: the "imports"
   uint64_t agreements_ = 0, map_failures_ = 0, closed_freed_ = 0;
+  uint64_t fallbacks_ = 0;  // calls that fell back because some rank could not map (warning rate)
   bool test_fake_ = false;
   bool warned_export_ = false;
   int sock_ = -1;          // this rank's datagram socket (abstract namespace), for descriptors
