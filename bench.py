@@ -683,10 +683,17 @@ def main():
         for _ in range(args.warmup):
             step()
         wall, ev_ms = timed(step, args.steps)
-        # every step of the job (1 + warmup + timed), recomputed by torch, compared bit for bit
+        # every step of the job (1 + warmup + timed), recomputed by torch, compared bit for bit;
+        # the recompute is timed too (events on torch's current stream, where add_ runs): the
+        # same bytes through PyTorch-ROCm's own element-wise kernel, for comparison
+        torch.cuda.synchronize()
+        t0e, t1e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0e.record()
         for _ in range(args.warmup + args.steps):
             ref.add_(b)
+        t1e.record()
         torch.cuda.synchronize()
+        torch_add_ms = t0e.elapsed_time(t1e) / (args.warmup + args.steps)
         exact_all = bool(torch.equal(a, ref))
         del ref, a0
         ms = wall / args.steps * 1e3
@@ -697,7 +704,10 @@ def main():
             "config": {"workload": f"1-GPU local reduce a <- a + b, 1 GiB {args.dtype} (BASELINE.md row '1-GPU local reduce')",
                        "count": count, "bytes": nbytes, "kernel": f"local_reduce_vec<{args.dtype},Sum>",
                        "parity_step_exact": exact, "parity_all_steps_exact": exact_all,
-                       "parity_check": "full buffer vs torch's own add repeated 1 + warmup + steps times"},
+                       "parity_check": "full buffer vs torch's own add repeated 1 + warmup + steps times",
+                       "torch_add": {"ms": round(torch_add_ms, 4),
+                                     "GBps": round(nbytes / (torch_add_ms / 1e3) / 1e9, 3),
+                                     "what": "the parity recompute a.add_(b): same bytes through torch's own kernel"}},
         })
         traffic, tsrc = pmc_traffic(f"local_reduce_{args.dtype}_1GiB")
         kern_key = "local_reduce_vec"
