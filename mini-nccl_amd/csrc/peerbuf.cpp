@@ -150,6 +150,11 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
     sockaddr_un a;
     unsigned len = 0;
     sock_addr(rank, &a, &len);
+    if (test_unreachable_ && len + 2 <= sizeof a) {  // CPU self-test: a name no peer sends to
+      a.sun_path[len - offsetof(sockaddr_un, sun_path)] = '-';
+      a.sun_path[len - offsetof(sockaddr_un, sun_path) + 1] = 'x';
+      len += 2;
+    }
     const int one = 1;  // the sender's credentials come with every datagram (checked in drain)
     if (sock_ < 0 || bind(sock_, (const sockaddr*)&a, (socklen_t)len) != 0 ||
         setsockopt(sock_, SOL_SOCKET, SO_PASSCRED, &one, sizeof one) != 0)
@@ -160,17 +165,66 @@ void PeerBuffers::init(Bootstrap& boot, int rank, int nranks, const std::vector<
   if (rank == 0 && names[0]) shm_unlink(names.data());
   bool all = true;
   for (int v : oks) all = all && v;
+  const char* off_why = "the ranks share no /dev/shm (per-call records)";
+  if (all) {
+    // every socket is bound: can every rank reach every rank of another process?  (Abstract
+    // sockets live in a network namespace: ranks in separate containers that share /dev/shm
+    // would otherwise fail their first call with new buffers instead of running the ring.)
+    int reach = hello(2.0) ? 1 : 0;
+    boot.allgather(&reach, oks.data(), sizeof reach);
+    for (int v : oks) all = all && v;
+    off_why = "a rank cannot reach its peers' descriptor sockets (separate network namespaces?)";
+  }
   if (!all) {
     if (m != MAP_FAILED) munmap(m, board_bytes_);
     if (sock_ >= 0) close(sock_);
     sock_ = -1;
+    for (Pending& p : pending_)
+      for (int i = 0; i < p.nfd; ++i) close(p.fd[i]);
+    pending_.clear();
     if (rank == 0)
-      fprintf(stderr, "[Mini-NCCL] warning: the ranks share no /dev/shm (per-call records): the read schedule is off "
-              "and every call runs the ring\n");
+      fprintf(stderr, "[Mini-NCCL] warning: %s: the read schedule is off and every call runs the ring\n", off_why);
     return;  // no board anywhere: the read schedule falls back on every rank
   }
   board_ = static_cast<Board*>(m);
   boot.barrier();  // the board is initialised before anyone negotiates
+}
+
+// Init: a datagram with no descriptors (call 0) to every rank of another process, and one from
+// each of them, within timeout_s.  False as soon as a peer's socket refuses (it is not in this
+// network namespace) or when the time is up.
+bool PeerBuffers::hello(double timeout_s) {
+  FdMsg m;
+  memset(&m, 0, sizeof m);
+  m.src = rank_;
+  std::vector<char> sent((size_t)nranks_, 0), heard((size_t)nranks_, 0);
+  for (int q = 0; q < nranks_; ++q)
+    if (q == rank_ || nonces_[(size_t)q] == nonces_[(size_t)rank_]) sent[(size_t)q] = heard[(size_t)q] = 1;
+  const double t0 = now_s();
+  for (int spins = 0;; ++spins) {
+    bool done = true;
+    for (int q = 0; q < nranks_; ++q) {
+      if (sent[(size_t)q]) continue;
+      const int rc = try_send(q, m, nullptr, 0);
+      if (rc < 0) return false;
+      sent[(size_t)q] = rc > 0;
+      done = done && rc > 0;
+    }
+    drain();
+    for (size_t i = 0; i < pending_.size();) {
+      if (pending_[i].k != 0) {
+        ++i;
+        continue;
+      }
+      heard[(size_t)pending_[i].src] = 1;
+      for (int j = 0; j < pending_[i].nfd; ++j) close(pending_[i].fd[j]);
+      pending_.erase(pending_.begin() + (long)i);
+    }
+    for (char h : heard) done = done && h;
+    if (done) return true;
+    if (now_s() - t0 > timeout_s) return false;
+    backoff(spins);
+  }
 }
 
 void PeerBuffers::reap() {

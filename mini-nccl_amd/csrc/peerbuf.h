@@ -85,6 +85,9 @@ class PeerBuffers {
     test_fake_ = fake;
     test_fail_call_ = fail_call;
   }
+  // CPU self-test (before init): bind this rank's socket under another name, as if it lived in
+  // another network namespace (its peers' datagrams are refused)
+  void set_test_unreachable(bool v) { test_unreachable_ = v; }
   // CPU self-test: report this rank's allocation (base, id) freed with its next record
   void test_report_freed(uint64_t base, uint64_t id) { freed_.emplace_back(base, id); }
 
@@ -106,6 +109,7 @@ class PeerBuffers {
   void sock_addr(int q, void* addr, unsigned* len) const;
   int try_send(int q, const FdMsg& m, const int* fds, int nfd);  // 1 sent, 0 queue full, -1 error
   bool drain();  // takes every datagram waiting on my socket into pending_; true if any
+  bool hello(double timeout_s);  // init: every rank of another process reachable both ways
   void send_fds(int q, const FdMsg& m, const int* fds, const WaitFn& wait_for);
   Pending take_fds(int q, uint64_t k, const WaitFn& wait_for);
 
@@ -135,6 +139,7 @@ class PeerBuffers {
   uint64_t agreements_ = 0, map_failures_ = 0, closed_freed_ = 0;
   uint64_t fallbacks_ = 0;  // calls that fell back because some rank could not map (warning rate)
   bool test_fake_ = false;
+  bool test_unreachable_ = false;
   bool warned_export_ = false;
   int sock_ = -1;          // this rank's datagram socket (abstract namespace), for descriptors
   std::string sock_base_;  // the communicator's socket names: <base>-r<rank>

@@ -431,6 +431,9 @@ int mnccl_board_selftest(int rank, int nranks, const char* ip, int port, int sce
     std::vector<uint64_t> nonces((size_t)nranks);
     for (int q = 0; q < nranks; ++q) nonces[(size_t)q] = 1000u + (uint64_t)q;  // one process per rank
     mnccl::PeerBuffers pb;
+    // scenario 7: the last rank's descriptor socket is out of its peers' reach (another network
+    // namespace): init must turn the read schedule off on EVERY rank (-3), within seconds
+    if (scenario == 7 && rank == nranks - 1) pb.set_test_unreachable(true);
     pb.init(b, rank, nranks, nonces, port);
     if (!pb.available()) return -3;
     // scenarios 4 / 5: every rank eligible with synthetic buffers (no HIP); 4: rank 1 cannot map

@@ -102,6 +102,21 @@ def test_read_schedule_rendezvous_across_processes(sim_lib, world, scenario):
             assert dec == exp, (r, dec)
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_read_schedule_off_when_a_socket_is_unreachable(sim_lib, world):
+    # csrc/peerbuf.cpp init: the ranks share the board but one rank's descriptor socket cannot be
+    # reached (as from another network namespace) -> the read schedule is off on EVERY rank (the
+    # self-test returns -3, "no board"), decided at init within the 2 s hello limit, instead of a
+    # failed first call with new buffers
+    import gpu_workers as GW
+    port = GW.free_port()
+    out = GW.run_ranks(_board_rank, world, lambda r: (r, world, port, 7, 4), 120)
+    assert sorted(out) == list(range(world)), out
+    for r in range(world):
+        assert "error" not in out[r], out[r].get("error")
+        assert out[r]["rc"] == -3 and out[r]["secs"] < 15, out[r]
+
+
 @pytest.mark.parametrize("world", [2, 4, 8, 16])
 @pytest.mark.parametrize("scenario", [4, 5, 6], ids=["map-failure", "reused-buffers", "freed-buffers"])
 def test_read_schedule_mapping_round(sim_lib, world, scenario):
