@@ -106,7 +106,7 @@ def test_read_schedule_rendezvous_across_processes(sim_lib, world, scenario):
 def test_read_schedule_off_when_a_socket_is_unreachable(sim_lib, world):
     # csrc/peerbuf.cpp init: the ranks share the board but one rank's descriptor socket cannot be
     # reached (as from another network namespace) -> the read schedule is off on EVERY rank (the
-    # self-test returns -3, "no board"), decided at init within the 2 s hello limit, instead of a
+    # self-test returns -3, "no board"), decided at init within the 10 s hello limit, instead of a
     # failed first call with new buffers
     import gpu_workers as GW
     port = GW.free_port()
@@ -114,7 +114,7 @@ def test_read_schedule_off_when_a_socket_is_unreachable(sim_lib, world):
     assert sorted(out) == list(range(world)), out
     for r in range(world):
         assert "error" not in out[r], out[r].get("error")
-        assert out[r]["rc"] == -3 and out[r]["secs"] < 15, out[r]
+        assert out[r]["rc"] == -3 and out[r]["secs"] < 30, out[r]
 
 
 @pytest.mark.parametrize("world", [2, 4, 8, 16])
