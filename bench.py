@@ -165,8 +165,9 @@ def fused_bytes(algo, esz, chunk, n):
     """Every byte one rank's fused kernel moves through its GPU's HBM per call (DESIGN.md,
     Kernels): ring / direct read each chunk of the input and write each of the output once,
     and 2(n-1) chunks land in and are read back from scratch: (6n - 4) chunks; read has no
-    scratch: input n, output n, plus the peers' n - 1 loads of this rank's result: 3n - 1."""
-    return esz * chunk * ((3 * n - 1) if algo == "read" else (6 * n - 4))
+    scratch: every chunk of the input read once (n - 1 of them by the peers) and every chunk of
+    the output written once (n - 1 of them by the peers' pushes): 2n."""
+    return esz * chunk * ((2 * n) if algo == "read" else (6 * n - 4))
 C4_SLICES = [65536, 131072, 262144, 1048576]
 C4_WINDOWS = [16, 32, 64]
 # 4 GiB fp32 per rank; MNCCL_BENCH_C4_MIB / MNCCL_BENCH_C4=1 rehearse the grid smaller / at n < 8

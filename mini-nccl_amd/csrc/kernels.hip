@@ -33,10 +33,11 @@
 //    consistent); nothing is reset per call and stale flags cannot satisfy a wait.
 //  * every spin is bounded (MINI_NCCL_TIMEOUT_MS via s_memrealtime) and also exits on
 //    the host abort word or a peer's ABORT; the kernel always terminates.
-//  * read_kernel loads the peers' user buffers with the same sc0 sc1 loads, after their START
-//    (their send is in memory: every kernel before the call ended and wrote its data back)
-//    or READY (their result slice was stored sc0 sc1 and drained before the flag); its own
-//    result slices are stored sc0 sc1 for the peers' loads.
+//  * read_kernel loads the peers' send buffers with the same sc0 sc1 loads, after their START
+//    (their send is in memory: every kernel before the call ended and wrote its data back),
+//    and pushes its result slices into their recv with sc0 sc1 stores (drained before DONE;
+//    the owner reads them only in later kernels, whose start makes them visible:
+//    profiles/r3_coherence_probe.txt).
 //  * MINI_NCCL_PULL=1 moves the slots to the sender's scratch (schedule.h slot_owner): the
 //    producer's sc0 sc1 stores stay local, the consumer's sc0 sc1 loads cross the link; the
 //    flags, credits and the drain-before-flag order are unchanged, and so is the argument
@@ -834,16 +835,38 @@ __device__ __forceinline__ void read_copy_wide(const CollParams& p, uint64_t sof
 #ifndef MNCCL_FOLD_ALL_MIN_N
 #define MNCCL_FOLD_ALL_MIN_N 2
 #endif
+// The read schedule's second half (MNCCL_READ_PUSH=1, the default): each rank pushes its result
+// slices into every peer's recv (sc0 sc1 stores, straight from the fold's registers) instead of
+// every rank loading them from the owners' recv after a READY -- no per-iteration READY, no copy
+// phase, and each GPU's HBM moves 2n chunks per call instead of 3n-1 (the result chunk is not
+// read back by the n-1 peers); DONE then also means "my pushes into your recv have landed", and
+// every rank waits for every peer's DONE before its kernel ends.  Only rank r ever writes chunk r
+// of any recv (in place: after its own loads of that slice).  Another process's writes into this
+// process's memory are visible to this process's next kernel (profiles/r3_coherence_probe.txt);
+// this rank never reads the pushed ranges inside the call.  On the one-GPU proxy: 1.1-1.45x the
+// load form at 2 / 4 / 8 ranks, 1 MiB - 1 GiB (profiles/r3_read_push_ab.txt).  =0 builds the load
+// form (READY per iteration, then every peer's result slice loaded over the links).
+#ifndef MNCCL_READ_PUSH
+#define MNCCL_READ_PUSH 1
+#endif
 
 template <typename T, int OPC, int G, int V>
 __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff, uint32_t nvec, int lane) {
   constexpr uint32_t S = 64 * V;
-  const int n = p.n, r = p.rank;
+  const int n = p.n, r = p.rank, w = wave_id().w;
   const uint32_t vb = nvec * 16;
   const rsrc_t loc = make_rsrc(p.send + coff, vb), out = make_rsrc(p.recv + coff, vb);
   rsrc_t in[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) in[g] = make_rsrc(p.peer_send[direct_peer(n, r, 1 + (g + 1 < n ? g : 0))] + coff, vb);
+  // MNCCL_READ_PUSH: the result also goes to the same offset of every peer's recv (pipeline w
+  // starts at peer w mod n-1, so a rank's pipelines spread their pushes over all links)
+  rsrc_t pout[MNCCL_READ_PUSH ? G : 1];
+  if (MNCCL_READ_PUSH) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      pout[g] = make_rsrc(p.peer_recv[direct_peer(n, r, 1 + (g + 1 < n ? (g + w) % (n - 1) : 0))] + coff, vb);
+  }
   v4u xa[G][V], aa[V], xb[G][V], ab[V];
   auto load = [&](v4u(&x)[G][V], v4u(&a)[V], uint32_t b) {
 #pragma unroll
@@ -864,6 +887,14 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
       }
 #pragma unroll
     for (int u = 0; u < V; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, a[u]);
+    if (MNCCL_READ_PUSH) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (g + 1 < n) {
+#pragma unroll
+          for (int u = 0; u < V; ++u) st_slot16(pout[g], (b + (uint32_t)(u * 64 + lane)) * 16, a[u]);
+        }
+    }
   };
   uint32_t b = 0;
   load(xa, aa, 0);
@@ -877,11 +908,12 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
   }
 }
 
+// Returns the leading bytes of the slice whose result it also pushed to the peers (MNCCL_READ_PUSH).
 template <typename T, int OPC, bool VEC>
-__device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, uint32_t nbytes, int lane) {
+__device__ __forceinline__ uint32_t read_fold(const CollParams& p, uint64_t coff, uint32_t nbytes, int lane) {
   if (!VEC) {
     read_fold_scalar<T, OPC>(p, coff, nbytes, lane, 0);
-    return;
+    return 0;
   }
   const int n = p.n, r = p.rank;
   const uint32_t nvec = nbytes >> 4;
@@ -895,7 +927,7 @@ __device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, ui
     else if (n <= 5) read_fold_all<T, OPC, 4, 4 - h>(p, coff, nvec, lane);
     else read_fold_all<T, OPC, 7, 3 - h>(p, coff, nvec, lane);
     if (nbytes & 15u) read_fold_scalar<T, OPC>(p, coff, nbytes, lane, nvec * 16);
-    return;
+    return MNCCL_READ_PUSH ? nvec * 16 : 0;
   }
   constexpr int U = kReadFoldU;
   const rsrc_t out = make_rsrc(p.recv + coff, nbytes);
@@ -927,14 +959,35 @@ __device__ __forceinline__ void read_fold(const CollParams& p, uint64_t coff, ui
   }
   if (b < nvec) read_fold_wide<T, OPC>(p, coff, b, nvec, lane);
   if (nbytes & 15u) read_fold_scalar<T, OPC>(p, coff, nbytes, lane, nvec * 16);
+  return 0;
 }
 
-// Messages per (pair, pipeline) and call: START (my send is readable: the call began on my
-// stream), READY(t) for t < iters (my result slice of iteration t is in my recv), DONE (I no
-// longer read your buffers: your stream may go on).  Order per pipeline: START, F0, F1, G0, F2,
-// G1, ..., G(I-1), DONE -- the next fold's loads leave before this iteration's results are
-// awaited.  DONE also returns credits for every message (the scratch schedules' slot counters
-// continue across calls, whatever the schedule).
+// MNCCL_READ_PUSH, the forms that do not push as they fold: bytes [off0, nbytes) of my result
+// slice, read back from my recv (stored and drained) into every peer's recv
+template <typename T, bool VEC>
+__device__ __forceinline__ void read_push_rest(const CollParams& p, uint64_t coff, uint32_t nbytes, uint32_t off0,
+                                               int lane) {
+  const int n = p.n, r = p.rank;
+  const rsrc_t src = make_rsrc(p.recv + coff, nbytes);
+  // 16-byte vectors only where the buffers are dword-aligned (VEC), element by element otherwise
+  const uint32_t v0 = VEC ? (off0 + 15u) >> 4 : 0, v1 = VEC ? nbytes >> 4 : 0;
+  for (int k = 1; k < n; ++k) {
+    const rsrc_t dst = make_rsrc(p.peer_recv[direct_peer(n, r, k)] + coff, nbytes);
+    for (uint32_t i = v0 + (uint32_t)lane; i < v1; i += 64) st_slot16(dst, i * 16, ld_slot16(src, i * 16));
+    const uint32_t e0 = (v1 > v0 ? v1 * 16 : off0) / sizeof(T), ne = nbytes / sizeof(T);
+    for (uint32_t i = e0 + (uint32_t)lane; i < ne; i += 64)
+      Scal<sizeof(T)>::st(dst, i * (uint32_t)sizeof(T), Scal<sizeof(T)>::ld(src, i * (uint32_t)sizeof(T)));
+  }
+}
+
+// Messages per (pair, pipeline) and call: START (my send is readable and my recv writable: the
+// call began on my stream), then -- load form only -- READY(t) for t < iters (my result slice of
+// iteration t is in my recv), DONE (I no longer read your buffers, my pushes into your recv have
+// landed: your stream may go on).  Push form per pipeline: START, F0 F1 ... F(I-1), DONE.  Load
+// form: START, F0, F1, G0, F2, G1, ..., G(I-1), DONE -- the next fold's loads leave before this
+// iteration's results are awaited.  The READY word counts iters + 2 messages per call either way
+// (the push form jumps from START to DONE); DONE also returns credits for every message (the
+// scratch schedules' slot counters continue across calls, whatever the schedule).
 template <typename T, int OPC, bool VEC>
 __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(CollParams p) {
   signal_start(p);
@@ -967,12 +1020,20 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
       // F(j): fold my chunk's slice j from the peers' send buffers, store, drain, READY
       const u64 s = (u64)j * A + w;
       const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
-      if (len) read_fold<T, OPC, VEC>(p, (u64)r * p.chunk_bytes + s * p.slice_bytes, len, lane);
+      const u64 coff = (u64)r * p.chunk_bytes + s * p.slice_bytes;
+      const uint32_t pushed = len ? read_fold<T, OPC, VEC>(p, coff, len, lane) : 0;
       drain_stores();
+      if (MNCCL_READ_PUSH) {
+        if (pushed < len) {
+          read_push_rest<T, VEC>(p, coff, len, pushed, lane);
+          drain_stores();
+        }
+        continue;  // no READY: the peers wait only for DONE
+      }
       if (p.sys_fence && lane == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + 2 + j);
     }
-    if (j > 0) {
+    if (!MNCCL_READ_PUSH && j > 0) {
       // G(j-1): every peer's result slice j-1, peer by peer (pipeline w starts at peer w mod
       // n-1, so a rank's pipelines spread over all links), into my recv
       // (full batches peer by peer; the rest of the slice -- all of a short one -- for every
@@ -1005,8 +1066,10 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
         }
     }
   }
-  // DONE: every load of a peer's buffer has returned; then wait until nobody reads mine
+  // DONE: every load of a peer's buffer has returned (and every push into the peers' recv has
+  // landed); then wait until nobody reads mine (and every peer's pushes into mine have landed)
   drain_stores();
+  if (p.sys_fence && lane == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if (lane < n && lane != r) {
     st_sys(p.peer_mbox[lane] + mbox_credit(n, C, r, w), rx[lane] + mpc);
     st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + mpc);

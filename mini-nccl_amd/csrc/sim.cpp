@@ -173,12 +173,13 @@ bool direct_step(World& W, Prog& P) {
   return true;
 }
 
-// One step of the read schedule (kernels.hip read_kernel): stage 0 publishes START, 1 waits for
-// every peer's START, 2 runs the iterations (k == 0: fold of iteration it from the peers' send
-// buffers into recv, then READY; k >= 1: copy of peer k's result slice of iteration it-1 out of
-// its recv, after its READY), 3 publishes DONE (+ credits), 4 waits for every peer's DONE.
-// Every peer access reads the peer's own buffers (W.send / W.recv of that rank), so an in-place
-// call whose order were wrong would read overwritten data and fail the oracle comparison.
+// One step of the read schedule (kernels.hip read_kernel, push form: MNCCL_READ_PUSH): stage 0
+// publishes START, 1 waits for every peer's START, 2 runs one iteration per step (the fold of
+// slice it of chunk r from the peers' send buffers, stored into this rank's recv AND pushed into
+// every peer's recv at the same offset -- no READY), 3 publishes DONE (+ credits), 4 waits for
+// every peer's DONE.  Every peer access touches the peer's own buffers (W.send / W.recv of that
+// rank), so an in-place call whose order were wrong would read overwritten data and fail the
+// oracle comparison.
 bool read_step(World& W, Prog& P) {
   const int n = W.n, r = P.r, w = P.w;
   auto tx = [&](int d) { return W.tx_seq[r][(size_t)d * W.C + w]; };
@@ -197,39 +198,28 @@ bool read_step(World& W, Prog& P) {
       P.k = 0;
       return true;
     case 2: {
-      if (P.k == 0) {
-        if (P.it < W.iters) {
-          const uint64_t s = (uint64_t)P.it * W.A + w;
-          const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
-          const uint64_t coff = (uint64_t)r * W.chunk_bytes + s * W.slice;
-          const float* local = (const float*)((const char*)W.send[r] + coff);
-          float* out = (float*)((char*)W.recv[r] + coff);
-          for (uint64_t i = 0; i < len / 4; ++i) {
-            float acc = local[i];
-            for (int k = 1; k < n; ++k) {
-              const int q = direct_peer(n, r, k);
-              acc = apply(W.op, ((const float*)((const char*)W.send[q] + coff))[i], acc);
-            }
-            out[i] = acc;
-          }
-          for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx(direct_peer(n, r, k)) + 2 + P.it;
-        }
-        if (P.it > 0) P.k = 1;
-        else ++P.it;
-      } else {
-        const uint32_t t = P.it - 1;
-        const int q = direct_peer(n, r, 1 + (P.k - 1 + w) % (n - 1));
-        if (W.ready(r, q, w) < rx(q) + 2 + t) return false;
-        const uint64_t s = (uint64_t)t * W.A + w;
+      if (P.it < W.iters) {
+        const uint64_t s = (uint64_t)P.it * W.A + w;
         const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
-        const uint64_t coff = (uint64_t)q * W.chunk_bytes + s * W.slice;
-        memcpy((char*)W.recv[r] + coff, (const char*)W.recv[q] + coff, len);
-        if (++P.k == n) {
-          P.k = 0;
-          ++P.it;
+        const uint64_t coff = (uint64_t)r * W.chunk_bytes + s * W.slice;
+        const float* local = (const float*)((const char*)W.send[r] + coff);
+        std::vector<float> res((size_t)(len / 4));
+        for (uint64_t i = 0; i < len / 4; ++i) {
+          float acc = local[i];
+          for (int k = 1; k < n; ++k) {
+            const int q = direct_peer(n, r, k);
+            acc = apply(W.op, ((const float*)((const char*)W.send[q] + coff))[i], acc);
+          }
+          res[(size_t)i] = acc;
         }
+        // every load of the slice came first (in place, recv chunk r of a peer is its send chunk r)
+        if (len) {
+          memcpy((char*)W.recv[r] + coff, res.data(), (size_t)len);
+          for (int k = 1; k < n; ++k) memcpy((char*)W.recv[direct_peer(n, r, k)] + coff, res.data(), (size_t)len);
+        }
+        ++P.it;
       }
-      if (P.it > W.iters) P.j = 3;
+      if (P.it >= W.iters) P.j = 3;
       return true;
     }
     case 3:

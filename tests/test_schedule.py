@@ -184,12 +184,13 @@ def test_sim_read_needs_no_slots(oracle_lib, sim_lib):
 
 
 def test_read_message_counts(sim_lib):
-    # per pipeline and call: START, fold + (n-1) copies per iteration, DONE (publish + wait)
+    # per pipeline and call: START (publish + wait), one fold-and-push per iteration (push form:
+    # no READY, no copies), DONE (publish + wait)
     n, C = 4, 2
     xs = O.random_inputs(n, n * 64, "f32")
     _, steps = S.allreduce(xs, algo=2, slice_bytes=64, channels=C)
     iters = -(-(64 * 4 // 64) // C)
-    assert steps == n * C * (4 + iters + 1 + iters * (n - 1))
+    assert steps == n * C * (4 + iters)
 
 
 @pytest.mark.parametrize("chunk", [0, 4, 1000, 1 << 16, (1 << 20) + 12, 3 << 22, 1 << 27, 1 << 30])
@@ -217,7 +218,7 @@ def test_read_small_calls_run_only_the_pipelines_they_need(oracle_lib, sim_lib, 
     xs = O.random_inputs(n, count, "f32", seed=40 + n)
     ref = O.allreduce(xs, slice_bytes=64)
     _, steps = S.allreduce(xs, algo=2, slice_bytes=64, channels=C)
-    assert steps == n * 3 * (4 + 1 + 1 + (n - 1))  # iters = 1 on 3 pipelines
+    assert steps == n * 3 * (4 + 1)  # iters = 1 on 3 pipelines
     for seed in range(3):
         got, _ = S.allreduce(xs, slice_bytes=64, channels=C, algos=[2, 0, 2, 1, 2, 2, 0, 1, 2], seed=seed + 1)
         assert all(same_bits(g, e) for g, e in zip(got, ref))

@@ -39,7 +39,7 @@ def main():
     algos = sys.argv[4:] or ["ring", "direct"]
     base = os.path.join(ROOT, "gpurun_out", tag)
     def fused_of(algo):  # bench.py fused_bytes: read has no scratch
-        return 4 * (COUNT // n) * ((3 * n - 1) if algo == "read" else (6 * n - 4))
+        return 4 * (COUNT // n) * ((2 * n) if algo == "read" else (6 * n - 4))
     summ_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     summ = json.load(open(summ_path)) if os.path.exists(summ_path) else {}
     pmc_csv = os.path.join(ROOT, "profiles", f"{rnd}_proxy_pmc_n{n}.csv")
@@ -72,7 +72,7 @@ def main():
                 "dispatches": [len(fe), len(wr)],
                 "note": f"{n} ranks sharing ONE MI355X (proxy); rank 0 profiled (apps/bin/perf_test --sizes 1024, "
                         "default knobs); medians after the first 5 dispatches; fused bytes = 4 B x chunk x (6n-4) for "
-                        "ring / direct, x (3n-1) for read",
+                        "ring / direct, x 2n for read (push form)",
                 "source": f"profiles/{rnd}_proxy_pmc_n{n}.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate "
                           "passes; FETCH x2, KiB x1024)",
             }
