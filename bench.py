@@ -914,7 +914,9 @@ def main():
                 link["topology_rank0"] = {"error": str(e)[:120]}
         # each schedule's ceiling from the probed links (min over ranks): the ring moves
         # 2(n-1)/n of the buffer through one link, direct 2/n through each of n-1 links as
-        # stores, read the same 2/n per link as loads (the probe's mesh pull from user memory)
+        # stores, read the same 2/n per link direction, half as loads (its fold: the probe's mesh
+        # pull from user memory) and half as stores (its result pushes: the mesh push into user
+        # memory) -> n / (1/pull + 1/push)
         if args.same_device:
             # every "link" of the one-GPU rehearsal is this GPU's HBM, shared with the other ranks'
             # kernels: a schedule's rate over that is no link fraction (round 2 printed 1.43)
@@ -923,10 +925,11 @@ def main():
         elif "probe_next_GBps" in link:
             pv = link.get("probe_variants_GBps_per_link", {})
             pull = pv.get("mesh_pull_sys_user") or pv.get("mesh_pull_sys")
+            push = pv.get("mesh_push_sys_user") or link["probe_mesh_GBps_per_link"]
             ceil = {"ring": link["probe_next_GBps"] * n / (2 * (n - 1)),
                     "direct": link["probe_mesh_GBps_per_link"] * n / 2}
-            if pull:
-                ceil["read"] = pull * n / 2
+            if pull and push:
+                ceil["read"] = n / (1.0 / pull + 1.0 / push)
             link.update({f"{a}_ceiling_GBps": round(c, 2) for a, c in ceil.items()})
             for a, ptn in result["schedules"].items():
                 if a in ceil and "value" in ptn:
