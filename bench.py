@@ -811,7 +811,7 @@ def main():
 
         headline_why = ("the library default for device buffers (MINI_NCCL_ALGO=auto -> read: each rank folds its "
                         "chunk from the peers' send buffers over the links in the reference ring's association "
-                        "order, then loads the peers' results -- the same bits as the ring, 2/n of the buffer per "
+                        "order and pushes the result into every peer's recv -- the same bits as the ring, 2/n of the buffer per "
                         "link instead of 2(n-1)/n through one link); the north star's ring is measured first and "
                         "beside it in schedules.ring with its own roofline and link fractions"
                         if headline_algo == "read" else f"{headline_algo} ({'forced by --algo' if not auto_mode else 'auto'})")
