@@ -10,7 +10,8 @@
 //                 Default geometry: 256 one-wave workgroups = one pipeline per CU.
 //  direct_kernel  same association order, every peer link at once (schedule.h).
 //  read_kernel    the default: same association order, no scratch -- each rank loads its
-//                 peers' send / recv buffers over the links (mapped by Comm per allocation).
+//                 peers' send buffers over the links and pushes its results into their recv
+//                 buffers (mapped by Comm per allocation).
 //  local_reduce   the element-wise op alone: out = op(local, incoming), 16 B per lane.
 //
 // Memory-ordering protocol (cross-process, cross-device over xGMI):
@@ -714,10 +715,11 @@ aborted:
 
 // ---------------------------------------------------------------- read kernel
 // MINI_NCCL_ALGO=read (schedule.h): no scratch.  Comm maps every peer's send and recv buffers
-// (HIP IPC, negotiated per call); rank r folds slice s of its own chunk r straight from the
-// peers' send buffers (sc0 sc1 loads over the links, the direct schedule's fold order), stores
-// the result into its own recv with sc0 sc1 (write-through: the peers' loads see it once the
-// wave drained), raises READY, and copies every peer's result slice out of that peer's recv.
+// (dma-buf imports, negotiated per call); rank r folds slice s of its own chunk r straight from
+// the peers' send buffers (sc0 sc1 loads over the links, the direct schedule's fold order) and
+// stores the result into its own recv and (push form, the default) into every peer's recv with
+// sc0 sc1 stores; the load form instead raises READY and copies every peer's result slice out of
+// that peer's recv (MNCCL_READ_PUSH below).
 //
 // Fold of slice `nbytes` at byte `coff` of chunk r: acc = op(x_q, acc) in ring order.
 template <typename T, int OPC>

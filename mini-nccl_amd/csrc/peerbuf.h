@@ -1,6 +1,7 @@
 // peerbuf.h -- the read schedule's per-call rendezvous (MINI_NCCL_ALGO=read).
 //
-// The read schedule loads its peers' send and recv buffers directly (kernels.hip read_kernel),
+// The read schedule loads its peers' send buffers and stores into their recv buffers directly
+// (kernels.hip read_kernel),
 // so before each call every rank must know where its peers' buffers are mapped in its own
 // address space.  The reference exchanged IPC handles of the user buffers through rank 0 on
 // EVERY call over TCP and opened/closed them each time (RDMATransport.h:171-257).  Here:
