@@ -148,26 +148,33 @@ def cpu_ring_baseline(n, budget_s=4.0):
 # own communicator (the knobs are read at ncclCommInitRank, as the reference's Config).
 SWEEP_POINTS = [
     # (algo, knobs over the library defaults: 256 one-wave workgroups, 128 KiB slices, 2 slots,
-    #  no hand-off fences, overlapped direct phases, push)
-    ("read", {}), ("read", {"MINI_NCCL_SLICE_SIZE": 32768}), ("read", {"MINI_NCCL_SLICE_SIZE": 524288}),
+    #  no hand-off fences, the read schedule's push form)
+    ("read", {}), ("read", {"MINI_NCCL_READ_PUSH": 0}),  # the push form and its comparison form
+    ("read", {"MINI_NCCL_SLICE_SIZE": 32768}), ("read", {"MINI_NCCL_SLICE_SIZE": 524288}),
     ("read", {"MINI_NCCL_CHANNELS": 128}), ("read", {"MINI_NCCL_CHANNELS": 512}),
     ("read", {"MINI_NCCL_THREADS": 128}), ("read", {"MINI_NCCL_SYS_FENCE": 1}),
-    ("direct", {}), ("direct", {"MINI_NCCL_SLOTS": 4}), ("direct", {"MINI_NCCL_SLICE_SIZE": 524288}),
-    ("direct", {"MINI_NCCL_SLICE_SIZE": 65536}), ("direct", {"MINI_NCCL_SYS_FENCE": 1}),
     ("ring", {}), ("ring", {"MINI_NCCL_SLOTS": 4}), ("ring", {"MINI_NCCL_SLICE_SIZE": 524288}),
-    # slots in the sender's scratch, loaded over the link (pull) instead of stored into (push)
-    ("direct", {"MINI_NCCL_PULL": 1}), ("ring", {"MINI_NCCL_PULL": 1}),
+    ("ring", {"MINI_NCCL_SYS_FENCE": 1}),
 ]
-ALGO_NAMES = ("ring", "direct", "read")  # mncclAlgo_t order
+ALGO_IDS = {"ring": 0, "read": 2}  # mncclAlgo_t
+ALGO_NAMES = {v: k for k, v in ALGO_IDS.items()}
 
 
-def fused_bytes(algo, esz, chunk, n):
+def kernel_form(algo, read_push=1):
+    """The kernel a schedule launches: ring_kernel, or read_kernel in its push / load form
+    (template PUSH): what a PMC entry must have profiled to describe this line's kernel."""
+    return "ring" if algo == "ring" else ("read_push" if read_push else "read_load")
+
+
+def fused_bytes(form, esz, chunk, n):
     """Every byte one rank's fused kernel moves through its GPU's HBM per call (DESIGN.md,
-    Kernels): ring / direct read each chunk of the input and write each of the output once,
-    and 2(n-1) chunks land in and are read back from scratch: (6n - 4) chunks; read has no
-    scratch: every chunk of the input read once (n - 1 of them by the peers) and every chunk of
-    the output written once (n - 1 of them by the peers' pushes): 2n."""
-    return esz * chunk * ((2 * n) if algo == "read" else (6 * n - 4))
+    Kernels): the ring reads each chunk of the input and writes each of the output once, and
+    2(n-1) chunks land in and are read back from scratch: (6n - 4) chunks; read has no scratch:
+    push form, every chunk of the input read once (n - 1 of them by the peers) and every chunk of
+    the output written once (n - 1 of them by the peers' pushes): 2n; load form, the rank's own
+    result chunk is also read back by the n - 1 peers: 3n - 1."""
+    k = {"ring": 6 * n - 4, "read_push": 2 * n, "read_load": 3 * n - 1}[form]
+    return esz * chunk * k
 C4_SLICES = [65536, 131072, 262144, 1048576]
 C4_WINDOWS = [16, 32, 64]
 # 4 GiB fp32 per rank; MNCCL_BENCH_C4_MIB / MNCCL_BENCH_C4=1 rehearse the grid smaller / at n < 8
@@ -183,7 +190,7 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
     comm = None
     try:
         comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
-        comm.set_algo(ALGO_NAMES.index(algo))
+        comm.set_algo(ALGO_IDS[algo])
         st = torch.cuda.Stream(device=dev)
         send = torch.ones(count, device=dev, dtype=tdt)
         recv = torch.empty(count, device=dev, dtype=tdt)
@@ -204,7 +211,7 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
         ok = comm.async_error() == 0 and bool((recv == float(n)).all().item())
         ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, st, 1, dist.barrier)
         i = comm.info()
-        ok = ok and i["last_algo"] == ALGO_NAMES.index(algo)  # the point ran its own schedule
+        ok = ok and i["last_algo"] == ALGO_IDS[algo]  # the point ran its own schedule
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
         return {"GBps": round(count * esz / (dt / reps) / 1e9, 2), "ok": ok, "workgroups": i["channels"],
                 "pipelines": i["pipelines"], "slot_bytes": i["slot_bytes"], "scratch_MiB": i["scratch_bytes"] >> 20}
@@ -282,12 +289,12 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_po
                            "WINDOW x 16, at most 256 pipelines; scratch capped at MINI_NCCL_SCRATCH_MB (512): "
                            "(n-1) x pipelines x 2 x SLICE <= cap, so large slices run fewer pipelines "
                            "(csrc/schedule.h pipeline_geometry; each point reports its geometry)")
-        # the same 4 GiB with the library defaults (the read schedule) and with the direct one
-        for key, algo in (("c4_read_4GiB_defaults", "read"), ("c4_direct_4GiB_defaults", "direct")):
-            if rank == 0:
-                log(f"C4: {algo} defaults")
-            out[key] = sweep_point(M, torch, dist, dev, n, rank, {}, algo, C4_COUNT, 3, max_over_ranks)
-            on_point()
+        # the same 4 GiB with the library defaults (the read schedule)
+        if rank == 0:
+            log("C4: read defaults")
+        out["c4_read_4GiB_defaults"] = sweep_point(M, torch, dist, dev, n, rank, {}, "read", C4_COUNT, 3,
+                                                   max_over_ranks)
+        on_point()
         c4 = out["c4_ring_4GiB"] = []
         for w in C4_WINDOWS:
             for sl in C4_SLICES:
@@ -486,26 +493,26 @@ def peer_topology(dev, n, same_device):
     return out
 
 
-def calibration_record(comm):
-    """MINI_NCCL_CALIBRATE (off by default): what the measured choice decided, if it ran"""
-    if os.environ.get("MINI_NCCL_CALIBRATE", "0") in ("", "0"):
-        return "off (MINI_NCCL_CALIBRATE=0, the library default)"
-    i = comm.info()
-    if i["calib_choice"] < 0:
-        return "on, undecided"
-    return {"choice": ALGO_NAMES[i["calib_choice"]], "read_ms": round(i["calib_ms"][0], 4),
-            ALGO_NAMES[i["scratch_algo"]] + "_ms": round(i["calib_ms"][1], 4)}
-
-
-def pmc_traffic(key):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/pmc_summary.json)."""
+def pmc_traffic(key, form=None, fused=None):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/pmc_summary.json),
+    keyed by kernel form.  An entry is used only if it profiled the kernel this line timed: its
+    kernel_form must be `form` and its fused_algorithmic_bytes_per_launch must equal `fused` (the
+    bytes of the form timed here) -- so a line can never pair one kernel's time with another
+    kernel's bytes (VERDICT r3 #5).  (traffic, source) or (None, why)."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         d = json.load(open(p))
-        e = d.get(key)
-        return (e["hbm_bytes_per_launch"], e.get("source")) if e else (None, None)
-    except Exception:
+    except Exception as e:
+        return None, f"no PMC summary ({str(e)[:60]})"
+    e = d.get(key)
+    if not e:
         return None, None
+    if form is not None and e.get("kernel_form") != form:
+        return None, f"refused: {key} profiled kernel form {e.get('kernel_form')!r}, this line timed {form!r}"
+    if fused is not None and e.get("fused_algorithmic_bytes_per_launch") != fused:
+        return None, (f"refused: {key} describes {e.get('fused_algorithmic_bytes_per_launch')} fused bytes per launch, "
+                      f"the kernel timed here moves {fused}")
+    return e["hbm_bytes_per_launch"], e.get("source")
 
 
 EXTRAS_LIMIT_S = float(os.environ.get("MNCCL_BENCH_EXTRAS_S", "300"))
@@ -571,7 +578,7 @@ def main():
     ap.add_argument("--count", type=int, default=0, help="elements (default: 1 GiB of --dtype)")
     ap.add_argument("--dtype", choices=["f32", "bf16", "f16"], default="f32",
                     help="f32 = the headline; bf16/f16 = BASELINE.json configs[4] (C5)")
-    ap.add_argument("--algo", choices=["auto", "ring", "direct", "read"], default=os.environ.get("MINI_NCCL_ALGO", "auto"),
+    ap.add_argument("--algo", choices=["auto", "ring", "read"], default=os.environ.get("MINI_NCCL_ALGO", "auto"),
                     help="auto = the library default (read for device buffers; same bits whatever the schedule)")
     ap.add_argument("--no-alt", action="store_true", help="skip the extras: N>1 the second schedule and the RCCL reference, N=1 the host-inclusive rate")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -710,13 +717,13 @@ def main():
                                      "GBps": round(nbytes / (torch_add_ms / 1e3) / 1e9, 3),
                                      "what": "the parity recompute a.add_(b): same bytes through torch's own kernel"}},
         })
-        traffic, tsrc = pmc_traffic(f"local_reduce_{args.dtype}_1GiB")
+        traffic, tsrc = pmc_traffic(f"local_reduce_{args.dtype}_1GiB", "local_reduce", None)
         kern_key = "local_reduce_vec"
     else:
         comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
         info = comm.info()
         # the headline runs the library's default for device buffers (MINI_NCCL_ALGO=auto: the
-        # read schedule; the measured choice is off by default); --algo forces one schedule
+        # read schedule in its push form); --algo forces one schedule
         auto_mode = args.algo == "auto"
         if auto_mode:
             args.algo = ALGO_NAMES[info["algo"]]
@@ -735,7 +742,9 @@ def main():
 
         def inject(where):
             """MNCCL_BENCH_INJECT=<where>: rehearses the failure paths below (a GPU fault aborts the
-            process: the armed line must still come out)"""
+            process: the armed line must still come out).  Stages after the ring: run_read (the
+            headline), probe, standalone, rccl, sizes, host_buffers, sweep; <stage>_error raises
+            an ncclInternalError there instead"""
             if os.environ.get("MNCCL_BENCH_INJECT") == where and rank == 0:
                 log(f"injected abort at {where}")
                 os.abort()
@@ -743,7 +752,7 @@ def main():
                 raise M.NcclError(M.ncclInternalError, f"injected at {where} (MNCCL_BENCH_INJECT)")
 
         def run_algo(algo, auto=False):
-            comm.set_algo(M.ALGO_AUTO if auto else ALGO_NAMES.index(algo))
+            comm.set_algo(M.ALGO_AUTO if auto else ALGO_IDS[algo])
             inject(f"run_{algo}")
             step = make_step()
             recv.fill_(-1.0)
@@ -758,10 +767,7 @@ def main():
             ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream,
                                     barrier=dist.barrier)
             i = comm.info()
-            want = ALGO_NAMES.index(algo)
-            if auto and i["calib_choice"] >= 0:  # MINI_NCCL_CALIBRATE=1: the measured choice
-                want = i["calib_choice"]
-            ok = ok and i["last_algo"] == want  # the timed calls ran this schedule (no fallback)
+            ok = ok and i["last_algo"] == ALGO_IDS[algo]  # the timed calls ran this schedule (no fallback)
             send.fill_(1.0)
             ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
             return max_over_ranks(wall), max_over_ranks(ev_ms), ok
@@ -770,8 +776,9 @@ def main():
             """one schedule's measured line: algbw, its kernel's roofline fraction (SURVEY s8(d)
             sum bytes over the fused kernel's own time) and every byte it moves through HBM"""
             ms_ = wall / args.steps * 1e3
-            fused = fused_bytes(algo, esz, count // n, n)
-            return {"algo": algo, "value": round(nbytes / (ms_ / 1e3) / 1e9, 3), "ms_per_step": round(ms_, 4),
+            fused = fused_bytes(kernel_form(algo, info["read_push"]), esz, count // n, n)
+            return {"algo": algo, "kernel_form": kernel_form(algo, info["read_push"]),
+                    "value": round(nbytes / (ms_ / 1e3) / 1e9, 3), "ms_per_step": round(ms_, 4),
                     "kernel_ms": round(ev_ms, 4), "result_check": "ok" if ok else "FAILED",
                     "roofline": {"frac": round(sum_bytes / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                                  "fused_frac": round(fused / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -781,7 +788,7 @@ def main():
             """the line's headline fields from one schedule's measurement"""
             ms_ = wall / args.steps * 1e3
             bw = nbytes / (ms_ / 1e3) / 1e9
-            fused = fused_bytes(algo, esz, count // n, n)
+            fused = fused_bytes(kernel_form(algo, info["read_push"]), esz, count // n, n)
             fa = fused / (ev_ms / 1e3) / 1e9
             result.update({
                 "value": round(bw, 3),
@@ -794,11 +801,12 @@ def main():
                            "pipelines": info["pipelines"], "scratch_bytes": info["scratch_bytes"],
                            "ranks_on_device": info["ranks_on_device"],
                            "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
-                           "headline_schedule": headline_why, "calibration": calibration_record(comm)},
+                           "read_push": info["read_push"], "headline_schedule": headline_why},
                 "roofline": {"bound": "hbm", "achieved": round(sum_bytes / (ev_ms / 1e3) / 1e9, 2),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(sum_bytes / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                             "traffic": None, "kernel": f"{algo}_kernel", "kernel_ms": round(ev_ms, 4),
+                             "traffic": None, "kernel": f"{algo}_kernel", "kernel_form": kernel_form(algo, info["read_push"]),
+                             "kernel_ms": round(ev_ms, 4),
                              "alg_bytes_per_launch": sum_bytes, "fused_alg_bytes_per_launch": fused,
                              "fused_achieved": round(fa, 2), "fused_frac": round(fa / HBM_PEAK_GBS, 4)},
                 # the host path beside every N: the CPU ring, timed before the GPU was
@@ -813,7 +821,8 @@ def main():
                         "chunk from the peers' send buffers over the links in the reference ring's association "
                         "order and pushes the result into every peer's recv -- the same bits as the ring, 2/n of the buffer per "
                         "link instead of 2(n-1)/n through one link); the north star's ring is measured first and "
-                        "beside it in schedules.ring with its own roofline and link fractions"
+                        "beside it in schedules.ring with its own roofline and link fractions; headline_check "
+                        "states whether this line's own numbers uphold that default"
                         if headline_algo == "read" else f"{headline_algo} ({'forced by --algo' if not auto_mode else 'auto'})")
         # 0. a line exists before anything runs on the GPU: if the process dies (a GPU fault
         # aborts it), the armed line is printed
@@ -868,7 +877,7 @@ def main():
             arm(result)
         # 3. the other schedules on the same buffers (same bits), each its own labelled point
         if not args.no_alt:
-            for other in ("ring", "direct", "read"):
+            for other in ("ring", "read"):
                 if other in result["schedules"]:
                     continue
                 if rank == 0:
@@ -879,10 +888,21 @@ def main():
                     result["schedules"][other] = {"algo": other, "error": str(e)[:200]}
                 if rank == 0:
                     arm(result)
-            comm.set_algo(M.ALGO_AUTO if auto_mode else ALGO_NAMES.index(args.algo))
+            comm.set_algo(M.ALGO_AUTO if auto_mode else ALGO_IDS[args.algo])
+        # the rule behind the default, checked against this line's own numbers: read stays the
+        # library default while it moves the buffer at least as fast as the reference's ring
+        rd, rg = result["schedules"].get("read", {}), result["schedules"].get("ring", {})
+        if "value" in rd and "value" in rg:
+            result["config"]["headline_check"] = {
+                "rule": "read is the default while schedules.read.value >= schedules.ring.value (same buffers, "
+                        "same bits); otherwise this node should run MINI_NCCL_ALGO=ring",
+                "read_GBps": rd["value"], "ring_GBps": rg["value"], "read_over_ring": round(rd["value"] / rg["value"], 3),
+                "holds": rd["value"] >= rg["value"]}
+        if rank == 0:
+            arm(result)
         # 4. the xGMI roofline the schedules are bound by, after the schedules themselves: bytes
         # per link with the hot path's access forms, one link per rank (the ring's) and every link
-        # at once (direct's stores, read's loads)
+        # at once (read's loads and pushes)
         link = {}
         try:
             torch.cuda.synchronize()
@@ -913,10 +933,9 @@ def main():
             except Exception as e:
                 link["topology_rank0"] = {"error": str(e)[:120]}
         # each schedule's ceiling from the probed links (min over ranks): the ring moves
-        # 2(n-1)/n of the buffer through one link, direct 2/n through each of n-1 links as
-        # stores, read the same 2/n per link direction, half as loads (its fold: the probe's mesh
-        # pull from user memory) and half as stores (its result pushes: the mesh push into user
-        # memory) -> n / (1/pull + 1/push)
+        # 2(n-1)/n of the buffer through one link; read 2/n per link direction, half as loads (its
+        # fold: the probe's mesh pull from user memory) and half as stores (its result pushes: the
+        # mesh push into user memory) -> n / (1/pull + 1/push)
         if args.same_device:
             # every "link" of the one-GPU rehearsal is this GPU's HBM, shared with the other ranks'
             # kernels: a schedule's rate over that is no link fraction (round 2 printed 1.43)
@@ -926,8 +945,7 @@ def main():
             pv = link.get("probe_variants_GBps_per_link", {})
             pull = pv.get("mesh_pull_sys_user") or pv.get("mesh_pull_sys")
             push = pv.get("mesh_push_sys_user") or link["probe_mesh_GBps_per_link"]
-            ceil = {"ring": link["probe_next_GBps"] * n / (2 * (n - 1)),
-                    "direct": link["probe_mesh_GBps_per_link"] * n / 2}
+            ceil = {"ring": link["probe_next_GBps"] * n / (2 * (n - 1))}
             if pull and push:
                 ceil["read"] = n / (1.0 / pull + 1.0 / push)
             link.update({f"{a}_ceiling_GBps": round(c, 2) for a, c in ceil.items()})
@@ -939,9 +957,13 @@ def main():
         result["link"] = link
         if rank == 0:
             arm(result)
-        traffic, tsrc = pmc_traffic(f"{args.algo}_{args.dtype}_1GiB_n{n}" + ("_same_gpu" if args.same_device else ""))
+        form = kernel_form(args.algo, info["read_push"])
+        traffic, tsrc = pmc_traffic(f"{form}_{args.dtype}_1GiB_n{n}" + ("_same_gpu" if args.same_device else ""),
+                                    form, fused_bytes(form, esz, count // n, n))
         if traffic is not None:
             result["roofline"].update({"traffic": traffic, "traffic_source": tsrc})
+        elif tsrc:
+            result["roofline"]["traffic_note"] = tsrc
         kern_key = f"{args.algo}_kernel"
     if n == 1:
         achieved = alg_bytes / (ev_ms / 1e3) / 1e9
@@ -964,6 +986,7 @@ def main():
             if turn != rank:
                 continue
             try:
+                inject("standalone")
                 sh_ = stream.cuda_stream
                 ks = []
                 for i in range(25):
@@ -1022,6 +1045,7 @@ def main():
         if rank == 0:
             log("extras: RCCL reference")
         try:
+            inject("rccl")
             if args.same_device:
                 raise RuntimeError("skipped: every rank on one GPU (RCCL needs one GPU per rank)")
             import torch.distributed as dist_
@@ -1050,6 +1074,7 @@ def main():
         if rank == 0:
             log("extras: sizes")
         try:
+            inject("sizes")
             if args.dtype == "f32":
                 result["sizes"] = size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks)
         except Exception as e:
@@ -1061,7 +1086,11 @@ def main():
         if args.dtype == "f32":
             if rank == 0:
                 log("extras: host buffers")
-            result["host_buffers"] = host_buffer_rate(M, torch, dist, comm, stream, n, max_over_ranks)
+            try:
+                inject("host_buffers")
+                result["host_buffers"] = host_buffer_rate(M, torch, dist, comm, stream, n, max_over_ranks)
+            except M.NcclError as e:
+                result["host_buffers"] = {"error": str(e)[:200]}
             if rank == 0:
                 arm(result)
     if n > 1:
@@ -1070,6 +1099,7 @@ def main():
         if not args.no_sweep and args.dtype == "f32":
             t_sw = time.time()
             result["sweep"] = {}
+            inject("sweep")
             run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks,
                        with_c4=(n == 8 or os.environ.get("MNCCL_BENCH_C4") == "1"), out=result["sweep"],
                        on_point=(lambda: arm(result)) if rank == 0 else (lambda: None))

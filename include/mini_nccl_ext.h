@@ -13,7 +13,7 @@
  *                        call returns this error), like NCCL's ncclCommGetAsyncError.
  *   mncclCommGetInfo     resolved configuration of a communicator (mncclCommGetInfoV: the
  *                        caller states its struct's size, so an older caller is never
- *                        written past its end).
+ *                        written past its end; mncclCommGetInfo writes the pre-300 prefix).
  *   mncclCommSetAlgo     choose the schedule for later calls (same association order).
  *   mncclCommLinkProbe   measure the xGMI write bandwidth the schedules are bound by.
  */
@@ -26,27 +26,30 @@
 extern "C" {
 #endif
 
-/* mncclVersion() of the library this header describes; mncclCommInfo_t grew in 300; 301:
-   user buffers shared as dma-bufs, MINI_NCCL_TUNE removed (same layout) */
-#define MNCCL_VERSION 301
+/* mncclVersion() of the library this header describes, 10000*major + 100*minor + patch:
+   300 mncclCommInfo_t grew (mncclCommGetInfoV); 301 user buffers shared as dma-bufs,
+   MINI_NCCL_TUNE removed; 400 the direct schedule and MINI_NCCL_PULL / DIRECT_OVERLAP /
+   CALIBRATE / PIPE_DEPTH / MIN_SLICE / STAGE_HOST removed, MINI_NCCL_READ_PUSH added, the ring
+   runs only the pipelines a call's slices need, mncclCommInfo_t grew again (same prefix) */
+#define MNCCL_VERSION 400
 
 /* schedules; all produce bit-identical results (same fold order per element) */
 typedef enum {
-  mncclAlgoAuto = -1,  /* the library's default: read for device buffers it can share; with
-                          MINI_NCCL_CALIBRATE=1 (off by default) the first calls of at least
-                          MINI_NCCL_CALIBRATE_BYTES time read against the scratch schedule and
-                          later such calls run the faster */
+  mncclAlgoAuto = -1,  /* the library's default: read for device buffers every rank can share,
+                          the ring for every other call */
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
-  mncclAlgoDirect = 1, /* every peer pushes its slice of chunk c straight to rank c over its
-                          own xGMI link; c folds them in ring order c, c+1, ..., c-1 and
-                          pushes the result to every peer (only when chosen explicitly) */
+  mncclAlgoDirect = 1, /* removed in 400 (never faster than the ring); mncclCommSetAlgo and
+                          MINI_NCCL_ALGO reject it */
   mncclAlgoRead = 2    /* no scratch: rank c loads the peers' slices of chunk c straight from
-                          their send buffers (mapped per allocation, negotiated per call),
-                          folds them in the same order into its recv, and every peer loads
-                          the result from there; a call whose buffers some rank cannot share
-                          (host memory; an allocation at an address the process exported
-                          before, see csrc/ipcreg.h) runs the scratch schedule instead, on
-                          every rank alike */
+                          their send buffers (mapped per allocation, negotiated per call) and
+                          folds them in the same order.  Push form (the default,
+                          MINI_NCCL_READ_PUSH=1): rank c stores the result into its own recv
+                          AND into every peer's recv -- the peers write chunk c of YOUR recv
+                          during the call, and those writes are visible to your stream's work
+                          after the call.  Load form (MINI_NCCL_READ_PUSH=0): every peer loads
+                          the result from rank c's recv.  A call whose buffers some rank
+                          cannot share (host memory, a full export table) runs the ring
+                          instead, on every rank alike */
 } mncclAlgo_t;
 
 typedef struct {
@@ -62,10 +65,8 @@ typedef struct {
   int sys_fence;          /* MINI_NCCL_SYS_FENCE: system-scope release fence before each flag */
   double timeout_s;       /* MINI_NCCL_TIMEOUT_MS / 1000 */
   size_t scratch_bytes;   /* device scratch owned by this rank */
-  double tune_ms[2];      /* always 0 since 301 (round 1's init-time ring / direct timing,
-                             MINI_NCCL_TUNE, was removed: MINI_NCCL_CALIBRATE measures read
-                             against the scratch schedule on real calls instead); kept for
-                             the layout */
+  double tune_ms[2];      /* always 0 since 301 (MINI_NCCL_TUNE was removed); kept for the
+                             layout */
   int pipelines;          /* channels x threads / 64 */
   int ranks_on_device;    /* ranks of this communicator on this rank's GPU (itself included) */
   size_t slot_bytes;      /* largest payload per message (MINI_NCCL_SLICE_SIZE unless the
@@ -76,17 +77,23 @@ typedef struct {
   size_t peer_mappings;   /* peers' user allocations mapped into this process for the read
                              schedule (dma-buf imports of every communicator; csrc/ipcreg.h) */
   int scratch_algo;       /* the read schedule's fallback for calls whose buffers cannot be
-                             shared: the ring (direct only when forced by MINI_NCCL_ALGO) */
-  int calib_choice;       /* MINI_NCCL_CALIBRATE: schedule kept for large calls (mncclAlgo_t), -1
-                             while undecided or when calibration is off */
-  double calib_ms[2];     /* the timings it was decided on: read, scratch schedule (ms per call,
-                             max over ranks); 0 until decided */
+                             shared: always the ring (mncclAlgoRing) */
+  int calib_choice;       /* -1 since 400 (MINI_NCCL_CALIBRATE was removed); kept for the layout */
+  double calib_ms[2];     /* 0 since 400; kept for the layout */
   /* since 300 */
   unsigned long long ipc_open_failures;  /* user-buffer imports that failed in this process */
   unsigned long long read_map_failures;  /* read calls this rank could not map (call fell back) */
   unsigned long long read_rounds;        /* read calls that needed the mapping round */
   unsigned long long closed_freed;       /* imports closed because their owner freed them */
   size_t live_exports;                   /* this process's user allocations exported and alive */
+  /* since 400 */
+  unsigned long long cap_refusals;       /* exports / imports refused because this process holds
+                                            512 exports / 1024 imports already: each such call
+                                            ran the ring (warned once per process) */
+  unsigned long long liveness_queries;   /* pointer queries this process made to find freed
+                                            exports (per call: the call's own buffers + at most
+                                            4 others) */
+  int read_push;                         /* MINI_NCCL_READ_PUSH: 1 push form, 0 load form */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,
@@ -95,17 +102,18 @@ ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming
 ncclResult_t mncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError);
 
 ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info);
-/* writes min(size, sizeof(mncclCommInfo_t)) bytes: callers built against an older header pass
-   their struct's size */
+/* mncclCommGetInfo writes the pre-300 prefix only (up to ipc_open_failures), so a caller built
+   against an older header is never overrun; mncclCommGetInfoV writes min(size,
+   sizeof(mncclCommInfo_t)) bytes: callers pass their struct's size */
 ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* info, size_t size);
 
 /* every rank must make the same choice before its next all-reduce; mncclAlgoAuto restores the
-   default (and its calibration) */
+   default; mncclAlgoDirect -> ncclInvalidArgument (removed in 400) */
 ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo);
 
 /* Collective diagnostic: every rank streams `bytes` (0 = its whole scratch region) into the
  * next rank's scratch (allPeers bit 0 = 0: one xGMI link per rank, the ring's) or into every
- * peer's at once (bit 0 = 1: the mesh, the direct schedule's), `iters` times, with the hot
+ * peer's at once (bit 0 = 1: the mesh, the read schedule's), `iters` times, with the hot
  * path's store form; *gbps = bytes per second per destination link.  Further bits of allPeers
  * select variants for comparison: bits 1-2 = the remote accesses' cache policy (0 = the hot
  * path's sc0 sc1, 1 = non-temporal, 2 = default), bit 3 = pull (load from the peers' scratch

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime_api.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
+#include <cstddef>
 #include <cstdio>
 #include <exception>
 #include <new>
@@ -140,8 +141,11 @@ ncclResult_t mncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError) {
   return ncclSuccess;
 }
 
+// The legacy entry point writes the layout it was published with (before 300): a caller built
+// against an older header is never written past the end of its struct; mncclCommGetInfoV gives
+// the rest.
 ncclResult_t mncclCommGetInfo(ncclComm_t comm, mncclCommInfo_t* info) {
-  return mncclCommGetInfoV(comm, info, sizeof(mncclCommInfo_t));
+  return mncclCommGetInfoV(comm, info, offsetof(mncclCommInfo_t, ipc_open_failures));
 }
 
 ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
@@ -171,15 +175,17 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
   info->slot_bytes = c->wave_slice();
   info->last_algo = c->last_algo();
   info->peer_mappings = c->peer_mappings();
-  info->scratch_algo = c->scratch_algo();
-  info->calib_choice = c->calib_choice();
-  info->calib_ms[0] = c->calib_ms(0);
-  info->calib_ms[1] = c->calib_ms(1);
+  info->scratch_algo = mncclAlgoRing;  // the read schedule's fallback
+  info->calib_choice = -1;              // MINI_NCCL_CALIBRATE was removed in 400
+  info->calib_ms[0] = info->calib_ms[1] = 0.0;
   info->ipc_open_failures = mnccl::ipc::open_failures();
   info->read_map_failures = c->peer_buffers().map_failures();
   info->read_rounds = c->peer_buffers().agreements();
   info->closed_freed = c->peer_buffers().closed_freed();
   info->live_exports = mnccl::ipc::live_exports();
+  info->cap_refusals = mnccl::ipc::cap_refusals();
+  info->liveness_queries = mnccl::ipc::liveness_queries();
+  info->read_push = k.read_push;
   memcpy(out, &full, size < sizeof full ? size : sizeof full);
   return ncclSuccess;
 }
@@ -188,8 +194,8 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
 // schedules' messages share mailboxes and slots), as with any other communicator setting.
 ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo) {
   if (!comm) return ncclInvalidArgument;
-  if (algo != mncclAlgoRing && algo != mncclAlgoDirect && algo != mncclAlgoRead && algo != mncclAlgoAuto)
-    return ncclInvalidArgument;
+  // mncclAlgoDirect (1) was removed in 400: it never beat the ring on any measured setup
+  if (algo != mncclAlgoRing && algo != mncclAlgoRead && algo != mncclAlgoAuto) return ncclInvalidArgument;
   reinterpret_cast<Comm*>(comm)->set_algo(algo);
   return ncclSuccess;
 }
@@ -206,6 +212,6 @@ ncclResult_t mncclCommLinkProbe(ncclComm_t comm, int allPeers, size_t bytes, int
   }
 }
 
-int mncclVersion(void) { return MNCCL_VERSION; /* 0.3.0: mncclCommInfo_t grew, mncclCommGetInfoV; 0.3.1: dma-buf sharing, no MINI_NCCL_TUNE */ }
+int mncclVersion(void) { return MNCCL_VERSION; }
 
 }  // extern "C"

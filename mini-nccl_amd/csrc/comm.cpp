@@ -98,26 +98,20 @@ struct PeerInfo {
   uint64_t host, nonce, pci;  // nonce: same process <=> same nonce; pci: the physical GPU
   uint64_t slice, scratch_bytes, mbox_bytes, scratch_cap;
   int32_t channels, slots, threads, abi;
-  int32_t window, signal_batch, algo, pad1;
-  uint64_t min_slice;
-  int32_t depth, overlap, pull, calibrate;
-  uint64_t calibrate_bytes;
+  int32_t window, signal_batch, algo, read_push;
   hipIpcMemHandle_t scratch_h, mbox_h;
   uint64_t scratch_ptr, mbox_ptr;  // raw addresses (same-process ranks) / the allocations' bases
   uint64_t scratch_id, mbox_id;    // HIP allocation ids (the import registry's keys)
 };
-constexpr uint32_t kInfoMagic = 0x4d4e4933u;  // 'MNI3'
+constexpr uint32_t kInfoMagic = 0x4d4e4934u;  // 'MNI4' (4.0's record: a 3.x rank fails the check)
 
 }  // namespace
 
 Comm::Comm(int nranks, int rank, const std::string& ip) : rank_(rank), nranks_(nranks) {
   cfg_ = Config::from_env();
-  // auto: the read schedule (same bits; no scratch; each call falls back to a scratch schedule
-  // when some rank's buffers cannot be shared) -- the scratch schedule is decided from the
-  // peers' devices in exchange_and_map
+  // auto: the read schedule (same bits; no scratch; each call falls back to the ring when some
+  // rank's buffers cannot be shared)
   algo_ = cfg_.algo >= 0 ? cfg_.algo : 2;
-  algo_auto_ = cfg_.algo < 0;
-  scratch_algo_ = cfg_.algo == 1 ? 1 : 0;
   if (nranks > kMaxRanks) throw std::invalid_argument("nRanks > 16 is not supported on one node");
   geo_ = pipeline_geometry(nranks, cfg_.channels, cfg_.threads, cfg_.window_size, cfg_.signal_batch, cfg_.slots,
                            cfg_.slice_size, cfg_.scratch_cap);
@@ -187,16 +181,11 @@ void Comm::exchange_and_map() {
   me.channels = cfg_.channels;
   me.slots = cfg_.slots;
   me.threads = cfg_.threads;
-  me.abi = 2;
+  me.abi = 4;
   me.window = cfg_.window_size;
   me.signal_batch = cfg_.signal_batch;
   me.algo = cfg_.algo;
-  me.min_slice = cfg_.min_slice;
-  me.depth = cfg_.pipe_depth;
-  me.overlap = cfg_.direct_overlap;
-  me.pull = cfg_.pull;
-  me.calibrate = cfg_.calibrate;
-  me.calibrate_bytes = cfg_.calibrate_bytes;
+  me.read_push = cfg_.read_push;
   me.scratch_h = scratch_h_;
   me.mbox_h = mbox_h_;
   me.scratch_ptr = (uint64_t)(uintptr_t)scratch_;
@@ -214,30 +203,14 @@ void Comm::exchange_and_map() {
     // every knob that shapes the kernels' geometry, message protocol or init sequence must agree
     if (p.slice != me.slice || p.channels != me.channels || p.slots != me.slots || p.threads != me.threads ||
         p.window != me.window || p.signal_batch != me.signal_batch || p.scratch_cap != me.scratch_cap ||
-        p.min_slice != me.min_slice || p.depth != me.depth || p.overlap != me.overlap || p.pull != me.pull ||
-        p.algo != me.algo || p.abi != me.abi ||
-        p.calibrate != me.calibrate || p.calibrate_bytes != me.calibrate_bytes)
+        p.algo != me.algo || p.read_push != me.read_push || p.abi != me.abi)
       throw std::invalid_argument(
-          "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SIGNAL_BATCH / SLOTS / CHANNELS / THREADS / SCRATCH_MB / MIN_SLICE / "
-          "PIPE_DEPTH / DIRECT_OVERLAP / PULL / ALGO / CALIBRATE / CALIBRATE_BYTES differ between "
-          "ranks");
+          "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SIGNAL_BATCH / SLOTS / CHANNELS / THREADS / SCRATCH_MB / ALGO / "
+          "READ_PUSH differ between ranks");
   }
-  // the scratch schedule of MINI_NCCL_ALGO=auto / read (the read schedule's fallback for calls
-  // whose buffers cannot be shared): the reference's ring, on every rank.  `direct` (every link
-  // at once) stays a forced choice (MINI_NCCL_ALGO=direct / mncclCommSetAlgo) until a node has
-  // measured it against the ring: on a shared GPU it trails the ring by 10-30 % with the same
-  // bytes (profiles/r3_direct_incremental_wait_ab.txt), and no cross-GPU run exists yet
-  bool one_device = true;
   ranks_on_device_ = 0;
-  for (int q = 0; q < nranks_; ++q) {
-    if (all[(size_t)q].pci != all[0].pci) one_device = false;
+  for (int q = 0; q < nranks_; ++q)
     if (all[(size_t)q].pci == me.pci) ++ranks_on_device_;
-  }
-  if (cfg_.algo < 0 || cfg_.algo == 2) scratch_algo_ = 0;
-  // measured choice between read and the scratch schedule for large calls: by default where the
-  // links decide it (ranks on more than one GPU); on one GPU read always wins (it moves half the
-  // HBM bytes), so it is off there unless MINI_NCCL_CALIBRATE=1
-  calib_on_ = cfg_.calibrate == 1 || (cfg_.calibrate < 0 && !one_device);
   // Rank PROCESSES sharing this GPU: a persistent kernel waits for its peers' kernels, so all of
   // them must be resident at once; the GPU's scheduler maps a bounded number of processes and
   // hardware queues together, beyond which it time-slices and every hand-off waits for a turn
@@ -297,6 +270,13 @@ void Comm::exchange_and_map() {
   std::vector<uint64_t> nonces((size_t)nranks_);
   for (int q = 0; q < nranks_; ++q) nonces[(size_t)q] = all[(size_t)q].nonce;
   pbuf_.init(boot_, rank_, nranks_, nonces, cfg_.port);
+  // the peers in other processes, for the import lifecycle (ipcreg.h comm_opened / comm_closed)
+  for (int q = 0; q < nranks_; ++q)
+    if (all[(size_t)q].nonce != me.nonce &&
+        std::find(owners_.begin(), owners_.end(), all[(size_t)q].nonce) == owners_.end())
+      owners_.push_back(all[(size_t)q].nonce);
+  ipc::comm_opened(owners_);
+  registered_ = true;
 }
 
 Comm::~Comm() {
@@ -312,6 +292,11 @@ Comm::~Comm() {
     } catch (...) {
     }
   }
+  // this communicator's kernels are done (waited above): its imports of peers no other live
+  // communicator of this process talks to are closed, and the exports too if it was the last one
+  // (a failed communicator's peers may still read this process's memory: then keep everything)
+  if (registered_ && sticky_ == ncclSuccess) ipc::comm_closed(owners_);
+  registered_ = false;
   release();
 }
 
@@ -329,11 +314,6 @@ void Comm::release() {
   stage_ = nullptr;
   stage_bytes_ = 0;
   if (order_ev_) hipEventDestroy(order_ev_);
-  for (auto& pair : calib_ev_)
-    for (hipEvent_t& e : pair) {
-      if (e) hipEventDestroy(e);
-      e = nullptr;
-    }
   order_ev_ = nullptr;
   have_last_ = false;
   scratch_ = nullptr;
@@ -437,7 +417,7 @@ Comm::Reach Comm::reach(const void* p, const void** kernel_ptr, bool* local) con
     *local = a.type == hipMemoryTypeDevice && !a.isManaged && a.device == device_;
     return Reach::kDevice;
   }
-  if (a.type == hipMemoryTypeHost && a.devicePointer && !cfg_.stage_host) {
+  if (a.type == hipMemoryTypeHost && a.devicePointer) {
     // device address of p itself (devicePointer / hostPointer may name the allocation base)
     const char* hp = (const char*)(a.hostPointer ? a.hostPointer : p);
     *kernel_ptr = (const char*)a.devicePointer + ((const char*)p - hp);
@@ -477,12 +457,11 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.chunk_bytes = chunk_bytes;
   const int C = wave_channels();
   p.slot_bytes = wave_slice();
-  p.slice_bytes = algo == 2 ? read_slice(chunk_bytes, C, cfg_.slice_size, cfg_.min_slice,
-                                         cfg_.pipe_depth > 1 ? cfg_.pipe_depth : kReadDepth)
-                            : effective_slice(chunk_bytes, C, wave_slice(), cfg_.min_slice, cfg_.pipe_depth);
+  p.slice_bytes = algo == 2 ? read_slice(chunk_bytes, C, cfg_.slice_size, kMinSlice, kReadDepth)
+                            : effective_slice(chunk_bytes, C, wave_slice(), kMinSlice, 1);
   p.nslices = (chunk_bytes + p.slice_bytes - 1) / p.slice_bytes;
-  // the read kernel runs one pipeline per slice up to C (schedule.h read_pipelines)
-  const int A = algo == 2 ? read_pipelines(p.nslices, C, geo_.waves) : C;
+  // either kernel runs one pipeline per slice up to C (schedule.h call_pipelines)
+  const int A = call_pipelines(p.nslices, C, geo_.waves);
   p.iters = (uint32_t)((p.nslices + (uint64_t)A - 1) / (uint64_t)A);
   p.pipes = C;
   p.n = n;
@@ -504,13 +483,11 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.call_seq = seq;
   p.timeout_ticks = (uint64_t)(cfg_.timeout_ms * 1e5);  // s_memrealtime runs at 100 MHz
   p.sys_fence = cfg_.sys_fence;
-  p.direct_overlap = cfg_.direct_overlap;
-  p.pull = cfg_.pull;
+  p.read_push = cfg_.read_push;
   p.tail_bytes = tail_bytes;
-  const int nt = cfg_.threads, wg = algo == 2 ? A / geo_.waves : geo_.workgroups;
-  hipError_t e = algo == 2   ? launch_read(dtype, op, vec, wg, nt, p, stream)
-                 : algo == 1 ? launch_direct(dtype, op, vec, wg, nt, p, stream)
-                             : launch_ring(dtype, op, vec, wg, nt, p, stream);
+  const int nt = cfg_.threads, wg = A / geo_.waves;
+  hipError_t e = algo == 2 ? launch_read(dtype, op, vec, wg, nt, p, stream)
+                           : launch_ring(dtype, op, vec, wg, nt, p, stream);
   hip_check(e, "kernel launch");
   last_algo_ = algo;
 }
@@ -563,7 +540,7 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     // need no pointer query: device memory of this GPU
     bool local_s = false, local_r = false;
     const bool read_sched = algo_ == 2 && pbuf_.available();
-    if (read_sched) pbuf_.reap();
+    if (read_sched) pbuf_.reap(send, recv);
     const Reach rs = read_sched && pbuf_.known(send) ? (local_s = true, Reach::kDevice) : reach(send, &ksend, &local_s);
     const Reach rr = read_sched && pbuf_.known(recv) ? (local_r = true, Reach::kDevice)
                                                      : reach(recv, (const void**)&krecv, &local_r);
@@ -589,10 +566,9 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     // straddle 16-byte boundaries on the local side; each message's last len % 16 bytes go
     // element by element); element-wise path otherwise (2-byte types with odd chunks)
     bool vec = (((uintptr_t)ksend | (uintptr_t)krecv) % 4 == 0) && (chunk_bytes % 4 == 0);
-    int algo = algo_ == 2 ? scratch_algo_ : algo_;
+    int algo = 0;  // the ring unless every rank can share its buffers
     const char* psend[kMaxRanks] = {};
     const char* precv[kMaxRanks] = {};
-    int measure = -1;  // calibration: this call's kernel is timed as read (0) / scratch schedule (1)
     if (algo_ == 2 && pbuf_.available()) {
       // the read schedule: every rank takes part in the rendezvous, all decide alike (a captured
       // call reads through mappings its replays keep using: imports stay open until their owner
@@ -600,16 +576,11 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
       const bool eligible = ksend == send && krecv == recv && local_s && local_r;
       bool vec_all = false;
       PeerBuffers::Decision d = PeerBuffers::kFallback;
-      // large auto calls while the measured choice is open (the same predicate on every rank)
-      const bool large = calib_on_ && algo_auto_ && !capturing && bytes >= cfg_.calibrate_bytes;
-      const bool calib = large && calib_choice_ < 0;
-      float max_t[2] = {0.f, 0.f};
-      if (calib) poll_calibration();
       try {
         // a peer that does not reach the call within the watchdog's limit fails it, as the
         // kernel's own wait would (the reference's 10 s watchdog, mini_nccl.cu:200-214)
         d = pbuf_.negotiate(send, recv, eligible, count, dtype, op, cfg_.timeout_ms / 1000.0 + 2.0,
-                            [this] { wait_previous_call(); }, psend, precv, &vec_all, my_t_, max_t);
+                            [this] { wait_previous_call(); }, psend, precv, &vec_all);
       } catch (const PeerGaveUp& e) {
         // a peer's communicator died in an earlier rendezvous: as a peer's ABORT in the kernel
         fprintf(stderr, "[Mini-NCCL] rank %d: %s; communicator is no longer usable\n", rank_, e.what());
@@ -631,40 +602,12 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
       }
       if (d == PeerBuffers::kRead) {
         algo = 2;
-        if (calib) {
-          if (max_t[0] > 0.f && max_t[1] > 0.f) {
-            // every rank's timings are in: keep the scratch schedule only if it is clearly faster
-            calib_ms_[0] = max_t[0];
-            calib_ms_[1] = max_t[1];
-            calib_choice_ = max_t[1] < 0.97f * max_t[0] ? scratch_algo_ : 2;
-            if (cfg_.debug && rank_ == 0)
-              fprintf(stderr, "[Mini-NCCL] calibration: read %.3f ms, %s %.3f ms per call -> %s\n", max_t[0],
-                      scratch_algo_ ? "direct" : "ring", max_t[1], calib_choice_ == 2 ? "read" : "scratch schedule");
-          } else {
-            // large call 0: read (warms the peer mappings), 1: the scratch schedule (warms its
-            // remote scratch), 2: the scratch schedule timed, 3: read timed, then read until every
-            // rank's timings are in
-            measure = calib_large_ == 2 ? 1 : calib_large_ == 3 ? 0 : -1;
-            if (calib_large_ == 1 || calib_large_ == 2) algo = scratch_algo_;
-            ++calib_large_;
-          }
-        }
-        if (large && calib_choice_ >= 0) algo = calib_choice_;
-        if (algo == 2) vec = vec_all && (chunk_bytes % 4 == 0);
+        vec = vec_all && (chunk_bytes % 4 == 0);
       }
     }
     seq = ++call_seq_;
     if (seq == 0) seq = ++call_seq_;  // 0 = "no kernel" (wait_for)
-    if (measure >= 0) {
-      for (hipEvent_t& e : calib_ev_[measure])
-        if (!e) hip_check(hipEventCreate(&e), "calibration event");
-      hip_check(hipEventRecord(calib_ev_[measure][0], stream), "calibration event");
-    }
     launch(algo, ksend, krecv, chunk_bytes, dtype, op, stream, seq, vec, psend, precv, tail);
-    if (measure >= 0) {
-      hip_check(hipEventRecord(calib_ev_[measure][1], stream), "calibration event");
-      calib_rec_[measure] = true;
-    }
     if (rr == Reach::kStaged) hip_check(hipMemcpyAsync(recv, stage_, bytes, hipMemcpyDefault, stream), "stage out");
   }
   if (!capturing) {
@@ -675,18 +618,6 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
   if (cur_dev != device_) hipSetDevice(cur_dev);
   if (cfg_.blocking && cap == hipStreamCaptureStatusNone) return wait_for(stream, seq);
   return ncclSuccess;
-}
-
-void Comm::poll_calibration() {
-  for (int m = 0; m < 2; ++m) {
-    if (!calib_rec_[m] || my_t_[m] > 0.f) continue;
-    const hipError_t q = hipEventQuery(calib_ev_[m][1]);
-    if (q == hipErrorNotReady) continue;
-    float ms = 0.f;
-    if (q == hipSuccess && hipEventElapsedTime(&ms, calib_ev_[m][0], calib_ev_[m][1]) == hipSuccess)
-      my_t_[m] = ms > 1e-3f ? ms : 1e-3f;
-    (void)hipGetLastError();
-  }
 }
 
 void Comm::abort_peers() {

@@ -33,18 +33,11 @@ class Comm {
   int device() const { return device_; }
   const Config& config() const { return cfg_; }
   int algo() const { return algo_; }
-  // a < 0: the default (read, measured choice for large calls when calibration is on)
-  void set_algo(int a) {
-    algo_auto_ = a < 0;
-    algo_ = a < 0 ? 2 : a;
-  }
-  int calib_choice() const { return calib_choice_; }
-  double calib_ms(int i) const { return calib_ms_[i & 1]; }
+  // a < 0: the default (read for buffers every rank can share, the ring for the other calls)
+  void set_algo(int a) { algo_ = a < 0 ? 2 : a; }
   int last_algo() const { return last_algo_; }  // schedule of the last launched kernel, -1: none
   size_t peer_mappings() const { return pbuf_.mapped_allocations(); }
   const PeerBuffers& peer_buffers() const { return pbuf_; }
-  int scratch_algo() const { return scratch_algo_; }
-  // calibration of MINI_NCCL_ALGO=auto with MINI_NCCL_TUNE=1 (max over ranks, ms per call; 0 = not run)
   // rank processes / communicators whose GPU is this rank's GPU (this rank included)
   int ranks_on_device() const { return ranks_on_device_; }
   ncclResult_t async_error();
@@ -67,14 +60,12 @@ class Comm {
   enum class Reach { kDevice, kMapped, kStaged };
   Reach reach(const void* p, const void** kernel_ptr, bool* local) const;
   void ensure_stage(size_t bytes, hipStream_t stream);
-  // algo: 0 ring, 1 direct, 2 read (psend / precv: every rank's buffers mapped here)
+  // algo: 0 ring, 2 read (psend / precv: every rank's buffers mapped here)
   void launch(int algo, const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
               uint32_t seq, bool vec, const char* const* psend = nullptr, const char* const* precv = nullptr,
               size_t tail_bytes = 0);
   void wait_previous_call();
   ncclResult_t check_status();
-  // MINI_NCCL_CALIBRATE: read the timings of this rank's measured calls whose events completed
-  void poll_calibration();
   // a rank that gives up on a call outside its kernel (the read schedule's rendezvous) raises
   // every peer's ABORT word, as a timed-out kernel does, so the peers fail fast instead of
   // running into their own watchdog
@@ -83,20 +74,9 @@ class Comm {
   int rank_, nranks_, device_ = 0;
   Config cfg_;
   Geometry geo_;
-  int algo_ = 0;                 // 0 ring, 1 direct, 2 read
+  int algo_ = 0;                 // 0 ring, 2 read (its calls fall back to the ring when some rank's
+                                 // buffers cannot be shared)
   int last_algo_ = -1;
-  int scratch_algo_ = 0;         // ring or direct: the read schedule's fallback (and auto's rule)
-  // measured choice (MINI_NCCL_CALIBRATE): large auto calls 0-3 run read and the scratch
-  // schedule once each to warm up, then each once timed; every rank publishes its timings with
-  // its call records and all decide alike once every rank's are in
-  bool algo_auto_ = false;       // MINI_NCCL_ALGO=auto and no explicit mncclCommSetAlgo
-  bool calib_on_ = false;
-  int calib_large_ = 0;          // large auto calls so far (the same count on every rank)
-  int calib_choice_ = -1;        // schedule kept for large calls; -1 undecided
-  double calib_ms_[2] = {0.0, 0.0};
-  float my_t_[2] = {0.f, 0.f};   // this rank's timings: read, scratch schedule (ms; 0 unknown)
-  hipEvent_t calib_ev_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
-  bool calib_rec_[2] = {false, false};
   int ranks_on_device_ = 1;
   uint32_t call_seq_ = 0;        // kernel launches of this communicator (the kernel's start word)
   Bootstrap boot_;
@@ -114,6 +94,8 @@ class Comm {
   hipIpcMemHandle_t scratch_h_, mbox_h_;  // exported once (pool blocks, ipcreg.h)
   uint64_t scratch_id_ = 0, mbox_id_ = 0;
   PeerBuffers pbuf_;               // read schedule: per-call rendezvous + peers' buffer mappings
+  std::vector<uint64_t> owners_;   // process nonces of the peers in other processes
+  bool registered_ = false;        // ipc::comm_opened(owners_) done
 
   char* stage_ = nullptr;         // device staging copy for pageable host buffers (grown on demand)
   size_t stage_bytes_ = 0;

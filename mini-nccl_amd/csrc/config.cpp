@@ -58,25 +58,15 @@ Config Config::from_env() {
   const char* a = std::getenv("MINI_NCCL_ALGO");
   if (a && *a) {
     if (!strcmp(a, "ring")) c.algo = 0;
-    else if (!strcmp(a, "direct")) c.algo = 1;
     else if (!strcmp(a, "read")) c.algo = 2;
     else if (!strcmp(a, "auto")) c.algo = -1;
-    else throw std::invalid_argument(std::string("MINI_NCCL_ALGO=") + a + " (expected auto|ring|direct|read)");
+    else if (!strcmp(a, "direct"))  // round 1-3's third schedule: never faster than the ring, removed in 4.0
+      throw std::invalid_argument("MINI_NCCL_ALGO=direct is no longer built (4.0): use auto, ring or read");
+    else throw std::invalid_argument(std::string("MINI_NCCL_ALGO=") + a + " (expected auto|ring|read)");
   }
   c.blocking = env_int("MINI_NCCL_BLOCKING", 1) != 0;
   c.sys_fence = env_int("MINI_NCCL_SYS_FENCE", 0) != 0;
-  long long ms = env_int("MINI_NCCL_MIN_SLICE", 1024);
-  if (ms < 1024) ms = 1024;
-  c.min_slice = (size_t)((ms + 1023) & ~1023LL);
-  c.pipe_depth = (int)env_int("MINI_NCCL_PIPE_DEPTH", 1);
-  if (c.pipe_depth < 1) c.pipe_depth = 1;
-  c.direct_overlap = env_int("MINI_NCCL_DIRECT_OVERLAP", 1) != 0;
-  c.pull = env_int("MINI_NCCL_PULL", 0) != 0;
-  c.stage_host = env_int("MINI_NCCL_STAGE_HOST", 0) != 0;
-  if (const char* cal = std::getenv("MINI_NCCL_CALIBRATE"); cal && *cal)
-    c.calibrate = strcmp(cal, "auto") == 0 ? -1 : env_int("MINI_NCCL_CALIBRATE", 0) != 0 ? 1 : 0;
-  long long cb = env_int("MINI_NCCL_CALIBRATE_BYTES", 64LL << 20);
-  c.calibrate_bytes = (size_t)(cb < 1 ? 1 : cb);
+  c.read_push = env_int("MINI_NCCL_READ_PUSH", 1) != 0;
   c.timeout_ms = (double)env_int("MINI_NCCL_TIMEOUT_MS", 10000);
   if (c.timeout_ms < 1) c.timeout_ms = 1;
   c.port = (int)env_int("MINI_NCCL_PORT", 8888);
@@ -86,14 +76,12 @@ Config Config::from_env() {
 }
 
 std::string Config::describe() const {
-  char b[384];
+  char b[320];
   snprintf(b, sizeof b,
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, scratch_cap=%zu MiB, algo=%s, "
-           "blocking=%d, sys_fence=%d, min_slice=%zu, depth=%d, pull=%d, stage_host=%d, calibrate=%d (%zu B), "
-           "timeout=%.0f ms, port=%d",
+           "blocking=%d, sys_fence=%d, read_push=%d, timeout=%.0f ms, port=%d",
            slice_size, window_size, signal_batch, slots, channels, threads, scratch_cap >> 20,
-           algo < 0 ? "auto" : algo == 2 ? "read" : algo ? "direct" : "ring", blocking,
-           sys_fence, min_slice, pipe_depth, pull, stage_host, calibrate, calibrate_bytes, timeout_ms, port);
+           algo < 0 ? "auto" : algo == 2 ? "read" : "ring", blocking, sys_fence, read_push, timeout_ms, port);
   return b;
 }
 

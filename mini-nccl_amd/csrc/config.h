@@ -17,18 +17,12 @@ struct Config {
   int channels = 0;                // MINI_NCCL_CHANNELS workgroups (0 -> derived, Comm::geometry)
   size_t scratch_cap = 512u << 20; // MINI_NCCL_SCRATCH_MB cap on this rank's uncached scratch
   int threads = 64;                // MINI_NCCL_THREADS threads per workgroup (one pipeline per wave)
-  int algo = -1;                   // MINI_NCCL_ALGO    auto (-1) | ring (0) | direct (1) | read (2)
+  int algo = -1;                   // MINI_NCCL_ALGO    auto (-1) | ring (0) | read (2)
   int blocking = 1;                // MINI_NCCL_BLOCKING host waits for the stream (reference behaviour)
   int sys_fence = 0;               // MINI_NCCL_SYS_FENCE 1: system release / acquire fences around each hand-off
-  size_t min_slice = 1024;         // MINI_NCCL_MIN_SLICE smallest adaptive payload (>= SLICE_SIZE: adaptation off)
-  int pipe_depth = 1;              // MINI_NCCL_PIPE_DEPTH slices per pipeline targeted for small calls
-  int direct_overlap = 1;          // MINI_NCCL_DIRECT_OVERLAP next iteration's raw pushes before this one's results
-  int pull = 0;                    // MINI_NCCL_PULL   1: slots in the sender's scratch, loaded over the link
-  int stage_host = 0;              // MINI_NCCL_STAGE_HOST pinned host buffers: 0 = kernel maps them, 1 = staged copy
-  int calibrate = 0;               // MINI_NCCL_CALIBRATE auto algo: time read vs the scratch schedule on the first
-                                   //   large calls and keep the faster; 0 off (default: the scratch schedule has not
-                                   //   yet run across GPUs), 1 on, "auto" = when the ranks span >1 GPU
-  size_t calibrate_bytes = 64u << 20;  // MINI_NCCL_CALIBRATE_BYTES calls at least this large are timed / switched
+  int read_push = 1;               // MINI_NCCL_READ_PUSH read schedule: 1 = each rank pushes its result slices
+                                   //   into the peers' recv (default), 0 = the load form (every rank loads
+                                   //   the peers' results after a READY per iteration; the comparison form)
   double timeout_ms = 10000.0;     // MINI_NCCL_TIMEOUT_MS (reference watchdog: 10 s)
   int port = 8888;                 // MINI_NCCL_PORT   bootstrap port (reference: 8888)
   double bootstrap_timeout_ms = 60000.0;  // MINI_NCCL_BOOTSTRAP_TIMEOUT_MS

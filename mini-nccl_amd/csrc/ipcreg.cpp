@@ -52,6 +52,10 @@ struct State {
   std::vector<Block> pool;
   std::vector<std::pair<int, hsa_agent_t>> agents;  // HIP device ordinal -> its HSA agent
   uint64_t open_failures = 0;
+  uint64_t liveness_queries = 0, cap_refusals = 0;
+  size_t reap_cursor = 0;                            // next export the round-robin batch checks
+  std::vector<std::pair<uint64_t, int>> owner_refs;  // peer process nonce -> live communicators
+  int live_comms = 0;
 };
 
 State& st() {
@@ -162,6 +166,13 @@ bool export_allocation(uint64_t base, uint64_t id, uint64_t size, Shared* d, std
   }
   if (s.exports.size() >= kMaxExports) {
     if (why) *why = "this process holds " + std::to_string(kMaxExports) + " exports already";
+    ++s.cap_refusals;
+    static bool warned = false;  // once per process (under s.mu)
+    if (!warned) {
+      warned = true;
+      fprintf(stderr, "[Mini-NCCL] warning: this process shares %zu buffers with its peers already (the cap): calls "
+              "on buffers beyond it run the ring (counted in mncclCommInfo_t.cap_refusals)\n", kMaxExports);
+    }
     return false;
   }
   int fd = -1;
@@ -197,22 +208,46 @@ std::pair<uint64_t, uint64_t> freed_log_at(size_t i) {
   return s.freed.at(i);
 }
 
-void reap_freed_exports() {
+void reap_freed_exports(const uint64_t* addrs, int naddrs, size_t batch) {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
-  for (size_t i = 0; i < s.exports.size();) {
-    unsigned long long id = 0;
-    const hipError_t e = hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)s.exports[i].base);
-    if (e != hipSuccess || id != s.exports[i].id) {
-      (void)hipGetLastError();
-      // the peers' imports hold their own references: closing ours releases nothing they use
-      hsa_amd_portable_close_dmabuf(s.exports[i].d.fd);
-      s.freed.emplace_back(s.exports[i].base, s.exports[i].id);
-      s.exports.erase(s.exports.begin() + (long)i);
+  const size_t n = s.exports.size();
+  if (!n) return;
+  std::vector<char> check(n, 0);
+  for (size_t i = 0; i < n; ++i)
+    for (int a = 0; a < naddrs; ++a)
+      if (addrs[a] >= s.exports[i].base && addrs[a] - s.exports[i].base < s.exports[i].size) check[i] = 1;
+  for (size_t k = 0; k < batch && k < n; ++k) check[(s.reap_cursor + k) % n] = 1;
+  s.reap_cursor = n ? (s.reap_cursor + batch) % n : 0;
+  // is the allocation at the export's base still the one exported (same HIP buffer id)?
+  std::vector<Export> keep;
+  keep.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    const Export& x = s.exports[i];
+    bool alive = true;
+    if (check[i]) {
+      unsigned long long id = 0;
+      ++s.liveness_queries;
+      const hipError_t e = hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)x.base);
+      alive = e == hipSuccess && id == x.id;
+      if (e != hipSuccess) (void)hipGetLastError();
+    }
+    if (alive) {
+      keep.push_back(x);
     } else {
-      ++i;
+      // the peers' imports hold their own references: closing ours releases nothing they use
+      hsa_amd_portable_close_dmabuf(x.d.fd);
+      s.freed.emplace_back(x.base, x.id);
     }
   }
+  s.exports.swap(keep);
+  if (s.reap_cursor >= s.exports.size()) s.reap_cursor = 0;
+}
+
+uint64_t liveness_queries() {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  return s.liveness_queries;
 }
 
 size_t live_exports() {
@@ -282,6 +317,68 @@ size_t imports() {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
   return s.imports.size();
+}
+
+void note_cap_refusal(const std::string& what) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  ++s.cap_refusals;
+  static bool warned = false;  // once per process (under s.mu)
+  if (!warned) {
+    warned = true;
+    fprintf(stderr, "[Mini-NCCL] warning: %s: calls on further peer buffers run the ring (counted in "
+            "mncclCommInfo_t.cap_refusals)\n", what.c_str());
+  }
+}
+
+uint64_t cap_refusals() {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  return s.cap_refusals;
+}
+
+void comm_opened(const std::vector<uint64_t>& owners) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  ++s.live_comms;
+  for (uint64_t o : owners) {
+    bool found = false;
+    for (auto& r : s.owner_refs)
+      if (r.first == o) {
+        ++r.second;
+        found = true;
+      }
+    if (!found) s.owner_refs.emplace_back(o, 1);
+  }
+}
+
+void comm_closed(const std::vector<uint64_t>& owners) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  if (s.live_comms > 0) --s.live_comms;
+  for (uint64_t o : owners)
+    for (size_t i = 0; i < s.owner_refs.size(); ++i) {
+      if (s.owner_refs[i].first != o) continue;
+      if (--s.owner_refs[i].second > 0) break;
+      s.owner_refs.erase(s.owner_refs.begin() + (long)i);
+      // no live communicator of this process talks to that owner any more: its imports go
+      for (size_t j = 0; j < s.imports.size();) {
+        if (s.imports[j].owner == o) {
+          hsa_amd_interop_unmap_buffer(s.imports[j].map);
+          s.imports.erase(s.imports.begin() + (long)j);
+        } else {
+          ++j;
+        }
+      }
+      break;
+    }
+  if (s.live_comms == 0) {
+    // no peer can import from this process any more (its communicators are gone with ours):
+    // the descriptors go, so a later free of any exported allocation releases its memory
+    for (const Export& x : s.exports) hsa_amd_portable_close_dmabuf(x.d.fd);
+    s.exports.clear();
+    s.reap_cursor = 0;
+  }
 }
 
 uint64_t open_failures() {

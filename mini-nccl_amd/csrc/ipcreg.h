@@ -44,9 +44,14 @@ struct Shared {
 bool export_allocation(uint64_t base, uint64_t id, uint64_t size, Shared* d, std::string* why = nullptr);
 // A live export (as of the last reap_freed_exports) holding address p, with no HIP call.
 bool find_live_export(uint64_t p, uint64_t* base, uint64_t* id, Shared* d);
-// Finds exports whose allocation has been freed (one pointer query per live export), closes their
-// descriptors and appends them to the process's freed log.
-void reap_freed_exports();
+// Finds exports whose allocation has been freed, closes their descriptors and appends them to
+// the process's freed log.  Checked: every export holding one of `addrs` (a call's own buffers:
+// a call must never publish the export of a freed allocation whose address a new one re-uses),
+// then `batch` more in round-robin order -- so a call costs 2 + batch pointer queries whatever
+// the number of live exports, and a freed allocation's export is found within
+// live_exports / batch calls (its memory is pinned until then).
+void reap_freed_exports(const uint64_t* addrs, int naddrs, size_t batch);
+uint64_t liveness_queries();  // pointer queries made by reap_freed_exports, process-wide
 // The freed log (base, id), append-only: every communicator reads it from its own cursor.
 size_t freed_log_size();
 std::pair<uint64_t, uint64_t> freed_log_at(size_t i);
@@ -63,6 +68,18 @@ char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shar
 bool close_import(uint64_t owner, uint64_t base, uint64_t id);
 size_t imports();
 uint64_t open_failures();  // user-buffer imports that failed in this process
+// Exports (kMaxExports, 512) and imports (peerbuf.cpp kMaxImports, 1024) are capped per process;
+// a refused one sends its call to the ring.  Counted here, warned about once per process.
+void note_cap_refusal(const std::string& what);
+uint64_t cap_refusals();
+
+// Communicator lifecycle.  Every live communicator registers the process nonces of its peers
+// in other processes; comm_closed (once no kernel of the closing communicator runs) closes this
+// process's imports of an owner no other live communicator shares, and -- when it was the last
+// live communicator of the process -- this process's exports too, so memory a caller frees
+// after its last communicator is gone is released at once (the dma-bufs held it).
+void comm_opened(const std::vector<uint64_t>& owners);
+void comm_closed(const std::vector<uint64_t>& owners);
 
 // --- communicator blocks (hipIpc), never freed while the process lives; a released block is
 // handed to the next communicator asking for the same size and flags.  *h: the block's handle.

@@ -9,7 +9,7 @@ namespace mnccl {
 enum DType : int { kI32 = 2, kF16 = 6, kF32 = 7, kF64 = 8, kBF16 = 9 };
 enum RedOp : int { kSum = 0, kProd = 1, kMax = 2, kMin = 3 };
 
-// Everything a ring / direct kernel needs; passed by value as the kernel argument.
+// Everything a ring / read kernel needs; passed by value as the kernel argument.
 struct CollParams {
   const char* send;        // this rank's input (device)
   char* recv;              // this rank's output (device; may equal send)
@@ -17,7 +17,7 @@ struct CollParams {
   uint64_t slice_bytes;    // payload bytes per channel message (<= slot_bytes)
   uint64_t slot_bytes;     // scratch slot stride (fixed per communicator: the configured slice)
   uint64_t nslices;        // ceil(chunk_bytes / slice_bytes)
-  uint32_t iters;          // ceil(nslices / channels): slices per channel
+  uint32_t iters;          // ceil(nslices / A): slices per pipeline of this call
   int32_t n, rank, nslots;
   char* scratch;           // this rank's scratch (regions per source rank)
   uint64_t* mbox;          // this rank's mailbox
@@ -31,10 +31,9 @@ struct CollParams {
   uint32_t call_seq;       // this launch's sequence number (Comm::wait_for's deadline starts here)
   uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
   int32_t sys_fence;       // system-scope release fence before each ready flag
-  int32_t direct_overlap;  // direct: next iteration's raw pushes before this one's results
-  int32_t pull;            // slots in the sender's scratch, loaded over the link (schedule.h)
-  int32_t pipes;           // the communicator's pipelines (mailbox / counter layout); the read
-                           // kernel's grid may run fewer (schedule.h read_pipelines)
+  int32_t read_push;       // read schedule: 1 push form, 0 load form (MINI_NCCL_READ_PUSH)
+  int32_t pipes;           // the communicator's pipelines (mailbox / scratch / counter layout);
+                           // a call's grid may run fewer (schedule.h call_pipelines)
   const char* peer_send[16];  // read schedule: every rank's send buffer, mapped here (own at [rank])
   const char* peer_recv[16];  // read schedule: every rank's recv buffer, mapped here
   uint64_t tail_bytes;        // bytes past n * chunk_bytes that the kernel copies send -> recv
@@ -47,8 +46,6 @@ constexpr int kMaxRanks = 16;
 // (checked by the caller).  vec = 16-byte path (all offsets 16-byte aligned).
 hipError_t launch_ring(int dtype, int op, bool vec, int channels, int threads,
                        const CollParams& p, hipStream_t stream);
-hipError_t launch_direct(int dtype, int op, bool vec, int channels, int threads,
-                         const CollParams& p, hipStream_t stream);
 hipError_t launch_read(int dtype, int op, bool vec, int channels, int threads,
                        const CollParams& p, hipStream_t stream);
 // out[i] = op(local[i], incoming[i]) for i < count

@@ -8,15 +8,14 @@
 //                 pipeline moves its slices through a `slots`-deep FIFO in the next
 //                 rank's scratch with epoch-free monotone flags and explicit credits.
 //                 Default geometry: 256 one-wave workgroups = one pipeline per CU.
-//  direct_kernel  same association order, every peer link at once (schedule.h).
 //  read_kernel    the default: same association order, no scratch -- each rank loads its
 //                 peers' send buffers over the links and pushes its results into their recv
 //                 buffers (mapped by Comm per allocation).
 //  local_reduce   the element-wise op alone: out = op(local, incoming), 16 B per lane.
 //
 // Memory-ordering protocol (cross-process, cross-device over xGMI):
-//  * everything another rank writes lives in THIS rank's scratch / mailbox, allocated
-//    hipDeviceMallocUncached: no cache of any agent keeps a copy of those lines;
+//  * everything another rank writes in the ring lives in THIS rank's scratch / mailbox,
+//    allocated hipDeviceMallocUncached: no cache of any agent keeps a copy of those lines;
 //  * payload stores to a peer's slot are sc0 sc1 16-byte buffer stores (the instruction a
 //    system-scope atomic store is; write-through, nothing left dirty in an L2); the wave
 //    drains (s_waitcnt vmcnt(0) in asm, so the compiler cannot drop it) and lane 0 stores
@@ -36,13 +35,14 @@
 //    the host abort word or a peer's ABORT; the kernel always terminates.
 //  * read_kernel loads the peers' send buffers with the same sc0 sc1 loads, after their START
 //    (their send is in memory: every kernel before the call ended and wrote its data back),
-//    and pushes its result slices into their recv with sc0 sc1 stores (drained before DONE;
-//    the owner reads them only in later kernels, whose start makes them visible:
-//    profiles/r3_coherence_probe.txt).
-//  * MINI_NCCL_PULL=1 moves the slots to the sender's scratch (schedule.h slot_owner): the
-//    producer's sc0 sc1 stores stay local, the consumer's sc0 sc1 loads cross the link; the
-//    flags, credits and the drain-before-flag order are unchanged, and so is the argument
-//    above (uncached memory, system-scope accesses on both sides).
+//    and pushes its result slices into their recv with sc0 sc1 stores, drained before DONE.
+//    Why the owner's later kernels then read the pushed bytes and not stale lines its L2 kept
+//    of recv from before the call: a write that reaches memory from a CU under another L2
+//    invalidates this L2's copy of the line, and an sc0 sc1 store is acknowledged only once it
+//    has reached memory (measured across the eight L2s of one MI355X with no kernel boundary:
+//    tools/probe_xcd_coherence.hip, profiles/r4_xcd_coherence.txt; DESIGN.md "Coherence of the
+//    pushes").  Plain or non-temporal stores would NOT do: they are acknowledged from the
+//    writer's L2 and the owner's stale line survives (same probe).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -162,11 +162,10 @@ template <> struct Scal<8> {
   }
 };
 
-// message `seq` from `src` to `dst` on pipeline w (schedule.h: push = receiver's scratch, pull =
-// sender's); peer_scratch[rank] is this rank's own scratch
+// message `seq` from `src` to `dst` on pipeline w: in the receiver's scratch (schedule.h
+// msg_slot_off); peer_scratch[rank] is this rank's own scratch
 __device__ __forceinline__ char* msg_slot(const CollParams& p, int C, int src, int dst, int w, u64 seq) {
-  return p.peer_scratch[slot_owner(p.pull, src, dst)] +
-         scratch_slot_off(C, p.nslots, p.slot_bytes, slot_region(p.pull, src, dst), w, seq);
+  return p.peer_scratch[dst] + msg_slot_off(C, p.nslots, p.slot_bytes, src, dst, w, seq);
 }
 
 // ---------------------------------------------------------------- bounded waits
@@ -396,7 +395,9 @@ template <typename T, int OPC, bool VEC>
 __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) ring_kernel(CollParams p) {
   signal_start(p);
   const WaveId id = wave_id();
-  const int lane = id.lane, w = id.w, C = id.C;
+  // C: the communicator's pipelines (mailbox, scratch and counter layout); A: the ones this call
+  // runs (its grid, schedule.h call_pipelines), slice s on pipeline s mod A
+  const int lane = id.lane, w = id.w, C = p.pipes, A = id.C;
   const int n = p.n, r = p.rank, K = p.nslots;
   copy_tail(p, w, lane);
   const int prev = mod_n(r - 1, n), next = mod_n(r + 1, n);
@@ -413,7 +414,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) ring_kernel(Col
   const int nops = ring_num_ops(n);
 
   for (uint32_t it = 0; it < p.iters; ++it) {
-    const u64 s = (u64)it * C + w;
+    const u64 s = (u64)it * A + w;
     const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
     const u64 soff = s * p.slice_bytes;
     const u64 itoff = (u64)it * mpi;
@@ -455,271 +456,15 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) ring_kernel(Col
   }
 }
 
-// ---------------------------------------------------------------- direct kernel
-// element-wise fold for elements [off0 / sizeof(T), nbytes / sizeof(T)) of the slice
-template <typename T, int OPC>
-__device__ __forceinline__ void fold_scalar(const CollParams& p, const char* lsrc, char* ldst, const u64* rx0,
-                                            const u64* tx1, uint32_t nbytes, int w, int C, int lane, uint32_t off0) {
-  const int n = p.n, r = p.rank;
-  typedef typename Scal<sizeof(T)>::U Us;
-  const uint32_t ne = nbytes / sizeof(T);
-  for (uint32_t i = off0 / sizeof(T) + lane; i < ne; i += 64) {
-    T acc = reinterpret_cast<const T*>(lsrc)[i];
-    for (int k = 1; k < n; ++k) {
-      const int q = direct_peer(n, r, k);
-      const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q]), nbytes);
-      const T x = __builtin_bit_cast(T, Scal<sizeof(T)>::ld(in, i * (uint32_t)sizeof(T)));
-      acc = Op<T, OPC>::f(x, acc);
-    }
-    reinterpret_cast<T*>(ldst)[i] = acc;
-    for (int k = 1; k < n; ++k) {
-      const int d = direct_peer(n, r, k);
-      const rsrc_t out = make_rsrc(msg_slot(p, C, r, d, w, tx1[d]), nbytes);
-      Scal<sizeof(T)>::st(out, i * (uint32_t)sizeof(T), __builtin_bit_cast(Us, acc));
-    }
-  }
-}
-
-#ifndef MNCCL_FOLD_U
-#define MNCCL_FOLD_U 8
-#endif
-constexpr int kFoldU = MNCCL_FOLD_U;  // vectors per lane per batch in the fold (as kU for moves)
-
-// Fold of the n-1 arriving slices of this rank's own chunk, software-pipelined by one
-// peer so two slot loads per vector are in flight; acc = op(x_q, acc) in ring order.
-// rx0[q]: sequence number of q's raw message for this slice; tx1[d]: of my result message to d.
-// The peers' READY words are awaited here, one peer at a time in ring order, just before the
-// first loads of that peer's slice: the fold of the first arrivals overlaps the wait for the
-// later ones (a slice waited for all n-1 hand-offs before any work: the direct schedule's gap to
-// the ring on a shared GPU, profiles/r2_direct_sweep_n4_same_gpu.txt).  False: aborted.
-template <typename T, int OPC, bool VEC>
-__device__ __forceinline__ bool fold_and_push(const CollParams& p, const Ctl& ctl, const char* lsrc, char* ldst,
-                                              const u64* rx0, const u64* tx1, uint32_t nbytes, int w, int C,
-                                              int lane) {
-  const int n = p.n, r = p.rank;
-  auto ready = [&](int k) {
-    const int q = direct_peer(n, r, k);
-    if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 1, ctl, lane)) return false;
-    acquire_sys(p.sys_fence);
-    return true;
-  };
-  int waited = 0;  // peers (in ring order) whose READY has been seen
-  if (VEC) {
-    constexpr int U = kFoldU;
-    const uint32_t nvec = nbytes >> 4;
-    uint32_t b = 0;
-    // full batches, no per-vector predicate: every lane has U loads per stream in flight
-    // (a predicated batch made the compiler wait on each load before issuing the next)
-    for (; b + 64 * U <= nvec; b += 64 * U) {
-      v4u acc[U], cur[U], nxt[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) acc[u] = ld_g16(lsrc + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16);
-      if (waited < 1) {
-        if (!ready(1)) return false;
-        waited = 1;
-      }
-      {
-        const int q = direct_peer(n, r, 1);
-        const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q]), nbytes);
-#pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
-      }
-      for (int k = 1; k < n; ++k) {
-        if (k + 1 < n) {
-          if (waited < k + 1) {
-            if (!ready(k + 1)) return false;
-            waited = k + 1;
-          }
-          const int q = direct_peer(n, r, k + 1);
-          const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q]), nbytes);
-#pragma unroll
-          for (int u = 0; u < U; ++u) nxt[u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc[u] = reduce16<T, OPC>(cur[u], acc[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) st_g16(ldst + (size_t)(b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
-      for (int k = 1; k < n; ++k) {
-        const int d = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));  // staggered like phase A
-        const rsrc_t out = make_rsrc(msg_slot(p, C, r, d, w, tx1[d]), nbytes);
-#pragma unroll
-        for (int u = 0; u < U; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, acc[u]);
-      }
-    }
-    // the rest: one vector per lane (every peer's READY first)
-    for (; waited < n - 1; ++waited)
-      if (!ready(waited + 1)) return false;
-    for (uint32_t i = b + (uint32_t)lane; i < nvec; i += 64) {
-      v4u acc = ld_g16(lsrc + (size_t)i * 16);
-      for (int k = 1; k < n; ++k) {
-        const int q = direct_peer(n, r, k);
-        const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q]), nbytes);
-        acc = reduce16<T, OPC>(ld_slot16(in, i * 16), acc);
-      }
-      st_g16(ldst + (size_t)i * 16, acc);
-      for (int k = 1; k < n; ++k) {
-        const int d = direct_peer(n, r, k);
-        const rsrc_t out = make_rsrc(msg_slot(p, C, r, d, w, tx1[d]), nbytes);
-        st_slot16(out, i * 16, acc);
-      }
-    }
-    if (nbytes & 15u) fold_scalar<T, OPC>(p, lsrc, ldst, rx0, tx1, nbytes, w, C, lane, nvec * 16);
-  } else {
-    for (; waited < n - 1; ++waited)
-      if (!ready(waited + 1)) return false;
-    fold_scalar<T, OPC>(p, lsrc, ldst, rx0, tx1, nbytes, w, C, lane, 0);
-  }
-  return true;
-}
-
 constexpr int kMaxWaves = kMaxThreads / 64;
-
-// Phase A's raw pushes are pure remote stores.  One vmcnt counts loads and stores in issue
-// order, so a batch's loads cannot be used before the previous batch's stores are acknowledged:
-// a wave keeps one batch of stores in flight.  Twice the moves' batch (16 KiB per wave) for the
-// one phase with no other outbound stream (phase B pushes n-1 batches per fold batch): +17 %
-// per wave into far memory (tools/far_store_probe.hip).
-#ifndef MNCCL_PUSH_U
-#define MNCCL_PUSH_U 16
-#endif
-constexpr int kPushU = MNCCL_PUSH_U;
-
-template <typename T, int OPC, bool VEC>
-__global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) direct_kernel(CollParams p) {
-  signal_start(p);
-  const WaveId id = wave_id();
-  const int lane = id.lane, w = id.w, C = id.C, wv = id.wv;
-  const int n = p.n, r = p.rank, K = p.nslots;
-  copy_tail(p, w, lane);
-  // per-wave rows: per-pair FIFO counters at call start, and this iteration's positions
-  __shared__ u64 s_tx[kMaxWaves][kMaxRanks], s_rx[kMaxWaves][kMaxRanks];
-  __shared__ u64 s_rx0[kMaxWaves][kMaxRanks], s_tx1[kMaxWaves][kMaxRanks];
-  u64* tx = s_tx[wv];
-  u64* rx = s_rx[wv];
-  u64* rx0 = s_rx0[wv];
-  u64* tx1 = s_tx1[wv];
-  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox};
-  const int mpi = direct_msgs_per_iter();
-  if (lane < n) {
-    tx[lane] = p.tx_seq[(u64)lane * C + w];
-    rx[lane] = p.rx_seq[(u64)lane * C + w];
-  }
-  __builtin_amdgcn_wave_barrier();
-
-  const uint32_t nsteps = 3 * p.iters;
-  for (uint32_t j = 0; j < nsteps; ++j) {
-    int phase;
-    uint32_t it;
-    direct_phase_at(j, p.iters, p.direct_overlap, &phase, &it);
-    const u64 s = (u64)it * C + w;
-    const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
-    const u64 soff = s * p.slice_bytes;
-    const u64 itoff = (u64)it * mpi;
-    if (lane < n) {
-      rx0[lane] = rx[lane] + itoff;
-      tx1[lane] = tx[lane] + itoff + 1;
-    }
-    __builtin_amdgcn_wave_barrier();
-
-    if (phase == 0) {
-      // Phase A: push my raw slice of chunk d to rank d, for every peer d; one drain for all
-      // n-1 pushes, then the n-1 READY flags.  Pipeline w starts at peer (w mod n-1): the
-      // pipelines of a rank spread over all n-1 xGMI links instead of marching through them
-      // one link at a time (the push order does not touch the fold order).
-      for (int k = 1; k < n; ++k) {
-        const int d = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));
-        const u64 seq0 = tx[d] + itoff;
-        if (seq0 + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, d, w), seq0 + 1 - K, ctl, lane))
-          goto aborted;
-        if (len) {
-          const rsrc_t out = make_rsrc(msg_slot(p, C, r, d, w, seq0), len);
-          const u64 coff = (u64)d * p.chunk_bytes + soff;
-          move<T, OPC, VEC, kSend, kPushU>(p.send + coff, nullptr, out, out, len, lane);
-        }
-      }
-      drain_stores();
-      if (lane == 0) {
-        if (p.sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        for (int k = 1; k < n; ++k) {
-          const int d = direct_peer(n, r, k);
-          st_sys(p.peer_mbox[d] + mbox_ready(C, r, w), tx[d] + itoff + 1);
-        }
-      }
-    } else if (phase == 1) {
-      // Phase B: slot credits of the result message at every peer; then the fold, which waits
-      // for the n-1 raw slices of my chunk one peer at a time as it reaches them; store; push
-      // the result everywhere.
-      for (int k = 1; k < n; ++k) {
-        const int q = direct_peer(n, r, k);
-        if (tx1[q] + 1 > (u64)K && !wave_wait_ge(p.mbox + mbox_credit(n, C, q, w), tx1[q] + 1 - K, ctl, lane))
-          goto aborted;
-      }
-      if (len) {
-        const u64 coff = (u64)r * p.chunk_bytes + soff;
-        if (!fold_and_push<T, OPC, VEC>(p, ctl, p.send + coff, p.recv + coff, rx0, tx1, len, w, C, lane))
-          goto aborted;
-      } else {
-        for (int k = 1; k < n; ++k) {  // an empty slice still consumes every peer's message
-          const int q = direct_peer(n, r, k);
-          if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 1, ctl, lane)) goto aborted;
-        }
-      }
-      drain_stores();
-      if (lane == 0) {
-        for (int k = 1; k < n; ++k) {
-          const int q = direct_peer(n, r, k);
-          st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), rx0[q] + 1);  // raw slot consumed
-        }
-        if (p.sys_fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        for (int k = 1; k < n; ++k) {
-          const int d = direct_peer(n, r, k);
-          st_sys(p.peer_mbox[d] + mbox_ready(C, r, w), tx1[d] + 1);
-        }
-      }
-    } else {
-      // Phase C: every peer's result slice, each copied as soon as its READY is seen (ring
-      // order), one drain, n-1 credits
-      for (int k = 1; k < n; ++k) {
-        const int q = direct_peer(n, r, k);
-        if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx0[q] + 2, ctl, lane)) goto aborted;
-        acquire_sys(p.sys_fence);
-        if (len) {
-          const rsrc_t in = make_rsrc(msg_slot(p, C, q, r, w, rx0[q] + 1), len);
-          const u64 coff = (u64)q * p.chunk_bytes + soff;
-          move<T, OPC, VEC, kCopy>(nullptr, p.recv + coff, in, in, len, lane);
-        }
-      }
-      drain_stores();
-      if (lane == 0) {
-        for (int k = 1; k < n; ++k) {
-          const int q = direct_peer(n, r, k);
-          st_sys(p.peer_mbox[q] + mbox_credit(n, C, r, w), rx0[q] + 2);
-        }
-      }
-    }
-  }
-  if (lane < n && lane != r) {
-    p.tx_seq[(u64)lane * C + w] = tx[lane] + (u64)p.iters * mpi;
-    p.rx_seq[(u64)lane * C + w] = rx[lane] + (u64)p.iters * mpi;
-  }
-  return;
-aborted:
-  if (lane == 0)
-    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), abort_word(p));
-}
 
 // ---------------------------------------------------------------- read kernel
 // MINI_NCCL_ALGO=read (schedule.h): no scratch.  Comm maps every peer's send and recv buffers
 // (dma-buf imports, negotiated per call); rank r folds slice s of its own chunk r straight from
-// the peers' send buffers (sc0 sc1 loads over the links, the direct schedule's fold order) and
-// stores the result into its own recv and (push form, the default) into every peer's recv with
-// sc0 sc1 stores; the load form instead raises READY and copies every peer's result slice out of
-// that peer's recv (MNCCL_READ_PUSH below).
+// the peers' send buffers (sc0 sc1 loads over the links, in ring order) and stores the result
+// into its own recv and (push form, the default) into every peer's recv with sc0 sc1 stores; the
+// load form (MINI_NCCL_READ_PUSH=0, template PUSH = false) instead raises READY and copies every
+// peer's result slice out of that peer's recv.
 //
 // Fold of slice `nbytes` at byte `coff` of chunk r: acc = op(x_q, acc) in ring order.
 template <typename T, int OPC>
@@ -837,22 +582,20 @@ __device__ __forceinline__ void read_copy_wide(const CollParams& p, uint64_t sof
 #ifndef MNCCL_FOLD_ALL_MIN_N
 #define MNCCL_FOLD_ALL_MIN_N 2
 #endif
-// The read schedule's second half (MNCCL_READ_PUSH=1, the default): each rank pushes its result
+// The read schedule's second half (PUSH, MINI_NCCL_READ_PUSH=1, the default): each rank pushes its result
 // slices into every peer's recv (sc0 sc1 stores, straight from the fold's registers) instead of
 // every rank loading them from the owners' recv after a READY -- no per-iteration READY, no copy
 // phase, and each GPU's HBM moves 2n chunks per call instead of 3n-1 (the result chunk is not
 // read back by the n-1 peers); DONE then also means "my pushes into your recv have landed", and
 // every rank waits for every peer's DONE before its kernel ends.  Only rank r ever writes chunk r
-// of any recv (in place: after its own loads of that slice).  Another process's writes into this
-// process's memory are visible to this process's next kernel (profiles/r3_coherence_probe.txt);
-// this rank never reads the pushed ranges inside the call.  On the one-GPU proxy: 1.1-1.45x the
-// load form at 2 / 4 / 8 ranks, 1 MiB - 1 GiB (profiles/r3_read_push_ab.txt).  =0 builds the load
-// form (READY per iteration, then every peer's result slice loaded over the links).
-#ifndef MNCCL_READ_PUSH
-#define MNCCL_READ_PUSH 1
-#endif
+// of any recv (in place: after its own loads of that slice).  The pushes are sc0 sc1 stores: each
+// is acknowledged once it reached the owner's memory, which drops any copy of the line the owner's
+// L2 kept (file header), and this rank never reads the pushed ranges inside the call.  On the
+// one-GPU proxy: 1.1-1.45x the load form at 2 / 4 / 8 ranks, 1 MiB - 1 GiB
+// (profiles/r3_read_push_ab.txt).  PUSH = false is the load form (READY per iteration, then every
+// peer's result slice loaded over the links), kept as the comparison form.
 
-template <typename T, int OPC, int G, int V>
+template <typename T, int OPC, int G, int V, bool PUSH>
 __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff, uint32_t nvec, int lane) {
   constexpr uint32_t S = 64 * V;
   const int n = p.n, r = p.rank, w = wave_id().w;
@@ -861,10 +604,10 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
   rsrc_t in[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) in[g] = make_rsrc(p.peer_send[direct_peer(n, r, 1 + (g + 1 < n ? g : 0))] + coff, vb);
-  // MNCCL_READ_PUSH: the result also goes to the same offset of every peer's recv (pipeline w
-  // starts at peer w mod n-1, so a rank's pipelines spread their pushes over all links)
-  rsrc_t pout[MNCCL_READ_PUSH ? G : 1];
-  if (MNCCL_READ_PUSH) {
+  // PUSH: the result also goes to the same offset of every peer's recv (pipeline w starts at
+  // peer w mod n-1, so a rank's pipelines spread their pushes over all links)
+  rsrc_t pout[PUSH ? G : 1];
+  if (PUSH) {
 #pragma unroll
     for (int g = 0; g < G; ++g)
       pout[g] = make_rsrc(p.peer_recv[direct_peer(n, r, 1 + (g + 1 < n ? (g + w) % (n - 1) : 0))] + coff, vb);
@@ -889,7 +632,7 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
       }
 #pragma unroll
     for (int u = 0; u < V; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, a[u]);
-    if (MNCCL_READ_PUSH) {
+    if (PUSH) {
 #pragma unroll
       for (int g = 0; g < G; ++g)
         if (g + 1 < n) {
@@ -910,8 +653,8 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
   }
 }
 
-// Returns the leading bytes of the slice whose result it also pushed to the peers (MNCCL_READ_PUSH).
-template <typename T, int OPC, bool VEC>
+// Returns the leading bytes of the slice whose result it also pushed to the peers (PUSH).
+template <typename T, int OPC, bool VEC, bool PUSH>
 __device__ __forceinline__ uint32_t read_fold(const CollParams& p, uint64_t coff, uint32_t nbytes, int lane) {
   if (!VEC) {
     read_fold_scalar<T, OPC>(p, coff, nbytes, lane, 0);
@@ -924,12 +667,12 @@ __device__ __forceinline__ uint32_t read_fold(const CollParams& p, uint64_t coff
     // variants within 256 registers without spilling)
     constexpr int h = sizeof(T) == 2 ? 1 : 0;
     if (!nvec) {
-    } else if (n == 2) read_fold_all<T, OPC, 1, 12 - 4 * h>(p, coff, nvec, lane);
-    else if (n == 3) read_fold_all<T, OPC, 2, 8 - 2 * h>(p, coff, nvec, lane);
-    else if (n <= 5) read_fold_all<T, OPC, 4, 4 - h>(p, coff, nvec, lane);
-    else read_fold_all<T, OPC, 7, 3 - h>(p, coff, nvec, lane);
+    } else if (n == 2) read_fold_all<T, OPC, 1, 12 - 4 * h, PUSH>(p, coff, nvec, lane);
+    else if (n == 3) read_fold_all<T, OPC, 2, 8 - 2 * h, PUSH>(p, coff, nvec, lane);
+    else if (n <= 5) read_fold_all<T, OPC, 4, 4 - h, PUSH>(p, coff, nvec, lane);
+    else read_fold_all<T, OPC, 7, 3 - h, PUSH>(p, coff, nvec, lane);
     if (nbytes & 15u) read_fold_scalar<T, OPC>(p, coff, nbytes, lane, nvec * 16);
-    return MNCCL_READ_PUSH ? nvec * 16 : 0;
+    return PUSH ? nvec * 16 : 0;
   }
   constexpr int U = kReadFoldU;
   const rsrc_t out = make_rsrc(p.recv + coff, nbytes);
@@ -964,7 +707,7 @@ __device__ __forceinline__ uint32_t read_fold(const CollParams& p, uint64_t coff
   return 0;
 }
 
-// MNCCL_READ_PUSH, the forms that do not push as they fold: bytes [off0, nbytes) of my result
+// PUSH, the forms that do not push as they fold: bytes [off0, nbytes) of my result
 // slice, read back from my recv (stored and drained) into every peer's recv
 template <typename T, bool VEC>
 __device__ __forceinline__ void read_push_rest(const CollParams& p, uint64_t coff, uint32_t nbytes, uint32_t off0,
@@ -990,7 +733,7 @@ __device__ __forceinline__ void read_push_rest(const CollParams& p, uint64_t cof
 // iteration's results are awaited.  The READY word counts iters + 2 messages per call either way
 // (the push form jumps from START to DONE); DONE also returns credits for every message (the
 // scratch schedules' slot counters continue across calls, whatever the schedule).
-template <typename T, int OPC, bool VEC>
+template <typename T, int OPC, bool VEC, bool PUSH>
 __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(CollParams p) {
   signal_start(p);
   const WaveId id = wave_id();
@@ -1023,9 +766,9 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
       const u64 s = (u64)j * A + w;
       const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
       const u64 coff = (u64)r * p.chunk_bytes + s * p.slice_bytes;
-      const uint32_t pushed = len ? read_fold<T, OPC, VEC>(p, coff, len, lane) : 0;
+      const uint32_t pushed = len ? read_fold<T, OPC, VEC, PUSH>(p, coff, len, lane) : 0;
       drain_stores();
-      if (MNCCL_READ_PUSH) {
+      if (PUSH) {
         if (pushed < len) {
           read_push_rest<T, VEC>(p, coff, len, pushed, lane);
           drain_stores();
@@ -1035,7 +778,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
       if (p.sys_fence && lane == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + 2 + j);
     }
-    if (!MNCCL_READ_PUSH && j > 0) {
+    if (!PUSH && j > 0) {
       // G(j-1): every peer's result slice j-1, peer by peer (pipeline w starts at peer w mod
       // n-1, so a rank's pipelines spread over all links), into my recv
       // (full batches peer by peer; the rest of the slice -- all of a short one -- for every
@@ -1227,32 +970,24 @@ static hipError_t ring_for_t(int op, bool vec, int C, int nt, const CollParams& 
 }
 
 template <typename T>
-static hipError_t direct_for_t(int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
-#define DIRECT_CASE(OPC)                                                                         \
-  case OPC:                                                                                      \
-    if (vec) hipLaunchKernelGGL((direct_kernel<T, OPC, true>), dim3(C), dim3(nt), 0, st, p);    \
-    else hipLaunchKernelGGL((direct_kernel<T, OPC, false>), dim3(C), dim3(nt), 0, st, p);       \
-    break;
-  switch (op) {
-    DIRECT_CASE(kSum) DIRECT_CASE(kProd) DIRECT_CASE(kMax) DIRECT_CASE(kMin)
-    default: return hipErrorInvalidValue;
-  }
-#undef DIRECT_CASE
-  return hipGetLastError();
-}
-
-template <typename T>
 static hipError_t read_for_t(int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
-#define READ_CASE(OPC)                                                                           \
-  case OPC:                                                                                      \
-    if (vec) hipLaunchKernelGGL((read_kernel<T, OPC, true>), dim3(C), dim3(nt), 0, st, p);      \
-    else hipLaunchKernelGGL((read_kernel<T, OPC, false>), dim3(C), dim3(nt), 0, st, p);         \
+#define READ_LAUNCH(OPC, V)                                                                          \
+  if (p.read_push) hipLaunchKernelGGL((read_kernel<T, OPC, V, true>), dim3(C), dim3(nt), 0, st, p); \
+  else hipLaunchKernelGGL((read_kernel<T, OPC, V, false>), dim3(C), dim3(nt), 0, st, p);
+#define READ_CASE(OPC)           \
+  case OPC:                      \
+    if (vec) {                   \
+      READ_LAUNCH(OPC, true)     \
+    } else {                     \
+      READ_LAUNCH(OPC, false)    \
+    }                            \
     break;
   switch (op) {
     READ_CASE(kSum) READ_CASE(kProd) READ_CASE(kMax) READ_CASE(kMin)
     default: return hipErrorInvalidValue;
   }
 #undef READ_CASE
+#undef READ_LAUNCH
   return hipGetLastError();
 }
 
@@ -1287,12 +1022,6 @@ static hipError_t local_for_t(int op, void* out, const void* a, const void* b, u
 
 hipError_t launch_ring(int dtype, int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
 #define M(T) return ring_for_t<T>(op, vec, C, nt, p, st)
-  MNCCL_DISPATCH_T(dtype, M)
-#undef M
-}
-
-hipError_t launch_direct(int dtype, int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
-#define M(T) return direct_for_t<T>(op, vec, C, nt, p, st)
   MNCCL_DISPATCH_T(dtype, M)
 #undef M
 }

@@ -26,8 +26,9 @@ namespace {
 constexpr uint32_t kBoardMagic = 0x4d4e4253u;  // 'MNBS'
 constexpr int kBoardDepth = 16;                // records per rank in flight (calls ahead of the slowest peer)
 constexpr int kMaxFreed = 8;                   // freed allocations one record reports (the rest: next calls)
-constexpr size_t kMaxImports = 1024;           // peer allocations mapped per process; beyond: scratch schedule
+constexpr size_t kMaxImports = 1024;           // peer allocations mapped per process; beyond: the ring
 constexpr size_t kMaxKnown = 4096;
+constexpr size_t kReapBatch = 4;               // other live exports checked for a free per call
 
 double now_s() {
   struct timespec ts;
@@ -53,7 +54,6 @@ struct alignas(64) CallRec {
   uint64_t count;
   int32_t dtype, op, eligible, aligned;
   BufDesc send, recv;
-  float t[2];  // this rank's calibration timings so far (Comm: read, scratch schedule; 0 = unknown)
   int32_t nfreed;
   uint64_t freed[kMaxFreed][2];  // (base, id) of this rank's exported allocations freed since its last record
   // second round (only when some rank may have to open a new mapping): the call whose mapping
@@ -227,11 +227,12 @@ bool PeerBuffers::hello(double timeout_s) {
   }
 }
 
-void PeerBuffers::reap() {
+void PeerBuffers::reap(const void* send, const void* recv) {
   // allocations this process exported and has freed since my last call: my peers close their
   // imports (the process's log: another communicator of this process may have found them)
   if (test_fake_) return;
-  ipc::reap_freed_exports();
+  const uint64_t addrs[2] = {(uint64_t)(uintptr_t)send, (uint64_t)(uintptr_t)recv};
+  ipc::reap_freed_exports(addrs, 2, kReapBatch);
   for (const size_t end = ipc::freed_log_size(); freed_cursor_ < end; ++freed_cursor_)
     freed_.push_back(ipc::freed_log_at(freed_cursor_));
 }
@@ -314,6 +315,7 @@ char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, int fd, const ipc
   if (ipc::imports() >= kMaxImports) {
     if (fd >= 0) close(fd);
     *why = "the process maps " + std::to_string(kMaxImports) + " peer allocations already";
+    ipc::note_cap_refusal(*why);
     return nullptr;
   }
   std::string w;
@@ -330,7 +332,7 @@ char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, int fd, const ipc
 PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv, bool eligible, uint64_t count,
                                              int dtype, int op, double timeout_s,
                                              const std::function<void()>& sync_previous, const char** psend,
-                                             const char** precv, bool* vec_all, const float* my_t, float* max_t) {
+                                             const char** precv, bool* vec_all) {
   const uint64_t k = ++seq_;
   const double t0 = now_s();
   // spins until ready() -- bounded by the peer q giving up and by the rendezvous limit
@@ -346,8 +348,7 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
     }
   };
   try {
-    return negotiate_body(k, send, recv, eligible, count, dtype, op, sync_previous, psend, precv, vec_all, my_t, max_t,
-                          wait_for);
+    return negotiate_body(k, send, recv, eligible, count, dtype, op, sync_previous, psend, precv, vec_all, wait_for);
   } catch (...) {
     // this rank gives up (a peer that never came or gave up itself): say so on the board, so
     // every peer waiting in a rendezvous with it fails at once instead of at its own limit (the
@@ -476,8 +477,7 @@ template <typename WaitFor>
 PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible,
                                                   uint64_t count, int dtype, int op,
                                                   const std::function<void()>& sync_previous, const char** psend,
-                                                  const char** precv, bool* vec_all, const float* my_t, float* max_t,
-                                                  const WaitFor& wait_for) {
+                                                  const char** precv, bool* vec_all, const WaitFor& wait_for) {
   auto wait = [&](const std::atomic<uint64_t>& v, uint64_t want, int q, const char* what) {
     wait_for([&] { return v.load(std::memory_order_acquire) >= want; }, q, what);
   };
@@ -503,8 +503,6 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
   me.aligned = ((sd.raw | rd.raw) % 4 == 0) ? 1 : 0;
   me.send = sd;
   me.recv = rd;
-  me.t[0] = my_t ? my_t[0] : 0.f;
-  me.t[1] = my_t ? my_t[1] : 0.f;
   me.nfreed = 0;
   while (!freed_.empty() && me.nfreed < kMaxFreed) {
     me.freed[me.nfreed][0] = freed_.front().first;
@@ -522,8 +520,6 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
     uint64_t freed[kMaxFreed][2];
   };
   std::vector<Seen> recs((size_t)nranks_);
-  float tmax[2] = {0.f, 0.f};
-  bool tall[2] = {true, true};
   for (int q = 0; q < nranks_; ++q) {
     const CallRec& c = board_->rec[q][slot];
     if (q != rank_) wait(c.seq, k, q, "reach");
@@ -537,14 +533,8 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
     s.recv = c.recv;
     s.nfreed = c.nfreed < 0 ? 0 : c.nfreed > kMaxFreed ? kMaxFreed : c.nfreed;
     memcpy(s.freed, c.freed, sizeof s.freed);
-    for (int i = 0; i < 2; ++i) {
-      tall[i] = tall[i] && c.t[i] > 0.f;
-      tmax[i] = c.t[i] > tmax[i] ? c.t[i] : tmax[i];
-    }
   }
   board_->consumed[rank_].v.store(k, std::memory_order_release);  // my copies are taken
-  if (max_t)  // every rank's timing known -> their max (what every rank reads alike), else 0
-    for (int i = 0; i < 2; ++i) max_t[i] = tall[i] ? tmax[i] : 0.f;
 
   // the peers' freed allocations: forget them (every rank alike) and close my imports of them.
   // The owner's call that used one last ended only after every peer's kernel was done with it
@@ -656,7 +646,7 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
     throw std::runtime_error("read schedule: a mapping of a known buffer is missing: " + why);
   Decision out = kRead;
   if (need_agree) {
-    // second round: every rank's mapping outcome; one failure -> the scratch schedule for this
+    // second round: every rank's mapping outcome; one failure -> the ring for this
     // call on every rank (same bits, no buffer of a peer is read)
     ++agreements_;
     CallRec& mine = board_->rec[rank_][slot];
@@ -673,7 +663,7 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
       // 2nd, 4th, 8th ... fallback, not at every call
       ++fallbacks_;
       if ((fallbacks_ & (fallbacks_ - 1)) == 0)
-        fprintf(stderr, "[Mini-NCCL] rank %d: all-reduce #%llu falls back to the scratch schedule (fallback %llu): rank "
+        fprintf(stderr, "[Mini-NCCL] rank %d: all-reduce #%llu falls back to the ring (fallback %llu): rank "
                 "%d could not map a peer's buffer%s%s\n", rank_, (unsigned long long)k,
                 (unsigned long long)fallbacks_, failed, why.empty() ? "" : ": ", why.c_str());
       out = kFallback;

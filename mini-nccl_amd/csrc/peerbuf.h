@@ -14,7 +14,7 @@
 //    the mapping until the owner reports the allocation freed (ipcreg.h: a dma-buf import keeps
 //    its memory alive and can never show another allocation, unlike round 2's hipIpc handles);
 //  * every rank reads the same records, so every rank takes the same decision: the read
-//    schedule when all ranks can, the communicator's scratch schedule otherwise, an error when
+//    schedule when all ranks can, the ring otherwise, an error when
 //    the ranks disagree on count / dtype / op.
 #pragma once
 #include <hip/hip_runtime_api.h>
@@ -61,15 +61,14 @@ class PeerBuffers {
   // every rank's buffers are dword-aligned.  `sync_previous` waits for this communicator's last
   // kernel (before a freed peer allocation's mapping is closed).  Throws std::runtime_error when
   // a peer does not arrive within timeout_s.
-  // my_t / max_t (optional): two timings this rank publishes with its record, and per timing
-  // the max over every rank's published value, or 0 while some rank's is still unknown (0).
   Decision negotiate(const void* send, const void* recv, bool eligible, uint64_t count, int dtype, int op,
                      double timeout_s, const std::function<void()>& sync_previous, const char** psend,
-                     const char** precv, bool* vec_all, const float* my_t = nullptr, float* max_t = nullptr);
+                     const char** precv, bool* vec_all);
 
-  // This rank's exported allocations freed since the last call are found (one pointer query per
-  // live export) and queued for its next record.  Call before known() in each call.
-  void reap();
+  // This rank's exported allocations freed since the last call are found and queued for its next
+  // record: every export holding send or recv is checked (so known() below cannot name a freed
+  // allocation's export), plus kReapBatch others (ipcreg.h).  Call before known() in each call.
+  void reap(const void* send, const void* recv);
   // p lies in one of this rank's live exported allocations (no HIP call): device memory of
   // this GPU that the read schedule can share
   bool known(const void* p) const;
@@ -104,7 +103,7 @@ class PeerBuffers {
   template <typename WaitFor>
   Decision negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible, uint64_t count, int dtype,
                           int op, const std::function<void()>& sync_previous, const char** psend, const char** precv,
-                          bool* vec_all, const float* my_t, float* max_t, const WaitFor& wait_for);
+                          bool* vec_all, const WaitFor& wait_for);
   bool describe(const void* p, uint64_t* base, uint64_t* id, ipc::Shared* d);
   char* map_peer(int q, uint64_t base, uint64_t id, int fd, const ipc::Shared& d, std::string* why);
   void sock_addr(int q, void* addr, unsigned* len) const;

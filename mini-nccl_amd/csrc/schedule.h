@@ -16,11 +16,10 @@
 //                  send_idx (r-1)-j+1), stores it to recv, forwards unless j == n-2.
 // Messages per channel iteration: 2(n-1) sent to r+1, 2(n-1) received from r-1.
 //
-// Direct (same fold order, all links): per slice, rank r pushes its raw slice of every
-// chunk d != r to rank d, folds the n-1 arriving slices of its own chunk in ring order
-// r, r+1, ..., r-1 (acc = op(x_q, acc): the visited rank's value is the LEFT/local
-// operand exactly as at rank q of the ring), stores and pushes the result to every peer,
-// and stores the n-1 results it receives.  Messages per pair and iteration: 2.
+// Read (the default for device buffers, same fold order, every link): rank r folds slice s of
+// its own chunk r straight from the peers' send buffers in ring order r, r+1, ..., r-1
+// (acc = op(x_q, acc): the visited rank's value is the LEFT/local operand exactly as at rank q
+// of the ring) and pushes the result into every peer's recv (kernels.hip read_kernel).
 #pragma once
 #include <stdint.h>
 
@@ -81,54 +80,31 @@ MNCCL_HD RingOp ring_op(int n, int r, int k) {
   return o;
 }
 
-// Direct schedule: peer order for pushes and for the fold.
+// Peer order of the read schedule's fold (ring order from r + 1) and of its pushes.
 MNCCL_HD int direct_peer(int n, int r, int k) { return mod_n(r + k, n); }  // k = 1..n-1
-MNCCL_HD int direct_msgs_per_iter() { return 2; }  // per (pair, channel): raw, then final
 
-// Read schedule (MINI_NCCL_ALGO=read): no scratch; the same fold as direct, but rank r loads
-// the peers' raw slices of chunk r straight from their send buffers and each peer's result
-// slice from that peer's recv (Comm maps the peers' buffers).  Messages per (pair, pipeline)
-// and call, all on the READY word: START, one per iteration (result slice ready), DONE.
+// Read schedule (MINI_NCCL_ALGO=read): no scratch; rank r loads the peers' raw slices of chunk
+// r straight from their send buffers and stores the result into every rank's recv (push form)
+// or each peer loads it from r's recv after a READY (load form, MINI_NCCL_READ_PUSH=0).
+// Messages per (pair, pipeline) and call, all on the READY word: START, one per iteration (load
+// form only; the push form skips them), DONE.
 MNCCL_HD uint64_t read_msgs_per_call(uint32_t iters) { return (uint64_t)iters + 2; }
 
-// Pipelines a read-schedule call runs: one per slice, up to all C of them, rounded up to whole
-// workgroups of `waves` pipelines.  The others sit the call out on every rank alike (a pure
-// function of the call's size and the rank-uniform geometry), so their per-pair counters stay
-// in step; a small call then dispatches, handshakes and drains a few waves, not C.  Slice s of
-// a call goes to pipeline s mod A (iteration s / A).
-MNCCL_HD int read_pipelines(uint64_t nslices, int C, int waves) {
+// Pipelines a call runs (ring and read alike): one per slice, up to all C of them, rounded up to
+// whole workgroups of `waves` pipelines.  The others sit the call out on every rank alike (a
+// pure function of the call's size and the rank-uniform geometry), so their per-pair counters
+// stay in step; a small call then dispatches, handshakes and drains a few waves, not C (the
+// reference moves only the slices that exist, mini_nccl.cu:112-115).  Slice s of a call goes
+// to pipeline s mod A (iteration s / A).
+MNCCL_HD int call_pipelines(uint64_t nslices, int C, int waves) {
   uint64_t a = nslices < (uint64_t)C ? nslices : (uint64_t)C;
   if (a == 0) a = 1;
   a = (a + (uint64_t)waves - 1) / (uint64_t)waves * (uint64_t)waves;
   return a < (uint64_t)C ? (int)a : C;
 }
 
-// Direct phases of one pipeline, in execution order: A(t) pushes raw slices of iteration t,
-// B(t) folds and pushes results, C(t) copies the arriving results.  Plain order A0 B0 C0 A1 B1
-// C1 ...; overlapped order A0 B0 A1 C0 B1 A2 C1 ... B(I-1) C(I-1): the next iteration's raw
-// pushes go out before this iteration's results are awaited, so a pipeline always has a
-// message in flight.  Deadlock-free with 2 slots: A(t+1) needs each peer's B(t) (the credit
-// for raw(t)), which needs only this rank's A(t) and C(t-1), both earlier in the order
-// (tests/test_schedule.py runs both orders under random interleavings).
-MNCCL_HD void direct_phase_at(uint32_t j, uint32_t iters, int overlap, int* phase, uint32_t* it) {
-  if (!overlap) {
-    *phase = (int)(j % 3);
-    *it = j / 3;
-    return;
-  }
-  if (j == 0) {
-    *phase = 0;
-    *it = 0;
-    return;
-  }
-  const uint32_t t = (j - 1) / 3, m = (j - 1) % 3;
-  if (m == 0) { *phase = 1; *it = t; }
-  else if (m == 1 && t + 1 < iters) { *phase = 0; *it = t + 1; }
-  else { *phase = 2; *it = t; }
-}
-
-// Slice geometry shared by both schedules: channel w owns slices w, w+C, w+2C, ...
-// of every chunk; message bytes of slice s (0 for the padding slices past the end, which
+// Slice geometry shared by both schedules: pipeline w of a call running A pipelines owns slices
+// w, w+A, w+2A, ... of every chunk; message bytes of slice s (0 for the padding slices past the end, which
 // still move flags so every channel sends the same number of messages).
 MNCCL_HD uint64_t slice_len(uint64_t chunk_bytes, uint64_t slice_bytes, uint64_t s) {
   const uint64_t off = s * slice_bytes;
@@ -139,11 +115,12 @@ MNCCL_HD uint64_t slice_len(uint64_t chunk_bytes, uint64_t slice_bytes, uint64_t
 
 // Payload bytes per message for one call: the configured slice for large chunks; for chunks
 // too small to give every channel `depth` slices of it, ceil(chunk / (C * depth)) rounded up
-// to whole waves of 16-byte vectors (1 KiB) and at least `min_slice`, so small all-reduces
+// to whole waves of 16-byte vectors (1 KiB) and at least `min_slice` (kMinSlice), so small all-reduces
 // still spread over every pipeline instead of queueing on a few.  A pure function of the
 // call's size and the (rank-uniform) config: every rank picks the same value.  Scratch slot
 // addresses keep the configured stride whatever the payload (scratch_slot_off), so calls of
 // different sizes never alias each other's slots.  Slicing never changes results.
+constexpr uint64_t kMinSlice = 1024;  // one 16-byte vector per lane of a wave
 MNCCL_HD uint64_t effective_slice(uint64_t chunk_bytes, int C, uint64_t slice, uint64_t min_slice, int depth) {
   if (min_slice >= slice || depth < 1) return slice;
   const uint64_t per = (uint64_t)C * (uint64_t)depth;
@@ -236,12 +213,11 @@ MNCCL_HD uint64_t mbox_credit(int n, int C, int dst, int w) { return ((uint64_t)
 MNCCL_HD uint64_t mbox_abort(int n, int C) { return (uint64_t)2 * n * C * kFlagStride; }
 MNCCL_HD uint64_t mbox_words(int n, int C) { return mbox_abort(n, C) + kFlagStride; }
 
-// Where message `seq` from rank `src` to rank `dst` (pipeline w) lives.  Push (default): in the
-// receiver's scratch, region src -- the sender's stores cross the link.  Pull
-// (MINI_NCCL_PULL=1): in the sender's own scratch, region dst -- the receiver's loads cross the
-// link.  Flags, credits and sequence numbers are the same either way.
-MNCCL_HD int slot_owner(int pull, int src, int dst) { return pull ? src : dst; }
-MNCCL_HD int slot_region(int pull, int src, int dst) { return region_index(slot_owner(pull, src, dst), pull ? dst : src); }
+// Where message `seq` from rank `src` to rank `dst` (pipeline w) lives: in the receiver's
+// scratch, region src -- the sender's stores cross the link.
+MNCCL_HD uint64_t msg_slot_off(int C, int slots, uint64_t slot_bytes, int src, int dst, int w, uint64_t seq) {
+  return scratch_slot_off(C, slots, slot_bytes, region_index(dst, src), w, seq);
+}
 
 // Kernel status bits (host-mapped status word)
 enum : uint32_t { kStatusTimeout = 1u, kStatusHostAbort = 2u, kStatusRemoteAbort = 4u };

@@ -1,4 +1,4 @@
-// sim.cpp -- host-side simulator of the ring / direct kernels' protocol, for the CPU test
+// sim.cpp -- host-side simulator of the ring / read kernels' protocol, for the CPU test
 // suite (no GPU).  Each (rank, channel) runs the same op sequence as kernels.hip, using the
 // same schedule.h index math, scratch layout and mailbox layout; a wait that is not
 // satisfied yields, and the scheduler round-robins over all programs.  It checks:
@@ -28,8 +28,9 @@ float apply(int op, float a, float b) {
 }
 
 struct World {
-  int n, C, K, op, algo, overlap = 1, pull = 0;
-  int A = 0;  // pipelines the current call runs (read: schedule.h read_pipelines; else C)
+  int n, C, K, op, algo;
+  int A = 0;  // pipelines the current call runs (schedule.h call_pipelines)
+  bool push = true;  // read schedule: push form (kernels.hip PUSH) or load form
   uint64_t slice, slot_bytes, chunk_bytes, nslices;  // payload per message, slot stride
   uint32_t iters;
   std::vector<const float*> send;
@@ -38,10 +39,9 @@ struct World {
   std::vector<std::vector<uint64_t>> mbox;    // per rank
   std::vector<std::vector<uint64_t>> tx_seq, rx_seq;  // per rank: [peer * C + w]
 
-  // message `seq` from src to dst on pipeline w (schedule.h: push / pull placement)
+  // message `seq` from src to dst on pipeline w (schedule.h msg_slot_off: the receiver's scratch)
   char* slot(int src, int dst, int w, uint64_t seq) {
-    return scratch[slot_owner(pull, src, dst)].data() +
-           scratch_slot_off(C, K, slot_bytes, slot_region(pull, src, dst), w, seq);
+    return scratch[dst].data() + msg_slot_off(C, K, slot_bytes, src, dst, w, seq);
   }
   uint64_t& ready(int owner, int src, int w) { return mbox[owner][mbox_ready(C, src, w)]; }
   uint64_t& credit(int owner, int dst, int w) { return mbox[owner][mbox_credit(n, C, dst, w)]; }
@@ -66,8 +66,8 @@ void do_move(int kind, int op, const float* local, const float* in, float* recv,
 struct Prog {
   int r, w;
   uint32_t it = 0;
-  int k = 0;      // ring: op index within the iteration; read: 0 = fold, 1..n-1 = copy from peer k
-  uint32_t j = 0; // direct: phase step (direct_phase_at); read: stage
+  int k = 0;      // ring: op index within the iteration; read (load form): 0 = fold, 1..n-1 = copy from peer k
+  uint32_t j = 0; // read: stage
   bool done = false;
 };
 
@@ -77,7 +77,7 @@ bool ring_step(World& W, Prog& P) {
   const int prev = mod_n(r - 1, n), next = mod_n(r + 1, n);
   const uint64_t tx_base = W.tx_seq[r][(size_t)next * W.C + w], rx_base = W.rx_seq[r][(size_t)prev * W.C + w];
   const int mpi = ring_msgs_per_iter(n);
-  const uint64_t s = (uint64_t)P.it * W.C + w;
+  const uint64_t s = (uint64_t)P.it * W.A + w;  // slice s on pipeline s mod A (kernels.hip ring_kernel)
   const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
   const uint64_t soff = s * W.slice;
   const uint64_t itoff = (uint64_t)P.it * mpi;
@@ -102,89 +102,41 @@ bool ring_step(World& W, Prog& P) {
   return true;
 }
 
-// One direct phase (kernels.hip direct_kernel): k == 0 phase A (all raw pushes, then all READY
-// flags), k == 1 phase B (fold + result pushes), k == 2 phase C (all result copies, then all
-// credits).  A phase publishes nothing until its end, as the kernel's single drain per phase.
-bool direct_step(World& W, Prog& P) {
-  const int n = W.n, r = P.r, w = P.w, K = W.K;
-  int phase;
-  uint32_t it;
-  direct_phase_at(P.j, W.iters, W.overlap, &phase, &it);
-  const uint64_t s = (uint64_t)it * W.C + w;
-  const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
-  const uint64_t soff = s * W.slice;
-  const uint64_t itoff = (uint64_t)it * direct_msgs_per_iter();
-  // per-pair FIFO positions: raw message of this iteration = +0, result = +1
-  auto tx0 = [&](int d) { return W.tx_seq[r][(size_t)d * W.C + w] + itoff; };
-  auto rx0 = [&](int q) { return W.rx_seq[r][(size_t)q * W.C + w] + itoff; };
-  if (phase == 0) {
-    for (int k = 1; k < n; ++k) {
-      const int d = direct_peer(n, r, k);
-      if (tx0(d) + 1 > (uint64_t)K && W.credit(r, d, w) < tx0(d) + 1 - K) return false;
-    }
-    for (int k = 1; k < n; ++k) {
-      const int d = direct_peer(n, r, k);
-      if (len) {
-        const uint64_t coff = (uint64_t)d * W.chunk_bytes + soff;
-        do_move(kSend, W.op, (const float*)((const char*)W.send[r] + coff), nullptr, nullptr,
-                (float*)W.slot(r, d, w, tx0(d)), len);
-      }
-    }
-    for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx0(direct_peer(n, r, k)) + 1;
-  } else if (phase == 1) {
-    for (int k = 1; k < n; ++k) {
-      const int q = direct_peer(n, r, k);
-      if (W.ready(r, q, w) < rx0(q) + 1) return false;
-      if (tx0(q) + 2 > (uint64_t)K && W.credit(r, q, w) < tx0(q) + 2 - K) return false;
-    }
-    if (len) {
-      const uint64_t coff = (uint64_t)r * W.chunk_bytes + soff;
-      const float* local = (const float*)((const char*)W.send[r] + coff);
-      float* recv = (float*)((char*)W.recv[r] + coff);
-      for (uint64_t i = 0; i < len / 4; ++i) {
-        float acc = local[i];
-        for (int k = 1; k < n; ++k) {
-          const int q = direct_peer(n, r, k);
-          acc = apply(W.op, ((const float*)W.slot(q, r, w, rx0(q)))[i], acc);
-        }
-        recv[i] = acc;
-        for (int k = 1; k < n; ++k) {
-          const int d = direct_peer(n, r, k);
-          ((float*)W.slot(r, d, w, tx0(d) + 1))[i] = acc;
-        }
-      }
-    }
-    for (int k = 1; k < n; ++k) W.credit(direct_peer(n, r, k), r, w) = rx0(direct_peer(n, r, k)) + 1;
-    for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx0(direct_peer(n, r, k)) + 2;
-  } else {
-    for (int k = 1; k < n; ++k)
-      if (W.ready(r, direct_peer(n, r, k), w) < rx0(direct_peer(n, r, k)) + 2) return false;
-    for (int k = 1; k < n; ++k) {
-      const int q = direct_peer(n, r, k);
-      if (len) {
-        const uint64_t coff = (uint64_t)q * W.chunk_bytes + soff;
-        do_move(kCopy, W.op, nullptr, (const float*)W.slot(q, r, w, rx0(q) + 1), (float*)((char*)W.recv[r] + coff),
-                nullptr, len);
-      }
-    }
-    for (int k = 1; k < n; ++k) W.credit(direct_peer(n, r, k), r, w) = rx0(direct_peer(n, r, k)) + 2;
-  }
-  if (++P.j == 3 * W.iters) P.done = true;
-  return true;
-}
-
-// One step of the read schedule (kernels.hip read_kernel, push form: MNCCL_READ_PUSH): stage 0
-// publishes START, 1 waits for every peer's START, 2 runs one iteration per step (the fold of
-// slice it of chunk r from the peers' send buffers, stored into this rank's recv AND pushed into
-// every peer's recv at the same offset -- no READY), 3 publishes DONE (+ credits), 4 waits for
-// every peer's DONE.  Every peer access touches the peer's own buffers (W.send / W.recv of that
-// rank), so an in-place call whose order were wrong would read overwritten data and fail the
-// oracle comparison.
+// One step of the read schedule (kernels.hip read_kernel): stage 0 publishes START, 1 waits for
+// every peer's START, 2 runs the iterations, 3 publishes DONE (+ credits), 4 waits for every
+// peer's DONE.  Push form (W.push): one step per iteration -- the fold of slice it of chunk r
+// from the peers' send buffers, stored into this rank's recv AND into every peer's recv at the
+// same offset, no READY.  Load form: the fold of iteration t stores into this rank's recv and
+// raises READY(t); then, one step per peer (pipeline w starts at peer w mod n-1), each peer's
+// result slice t-1 is copied out of that peer's recv once its READY(t-1) is seen.  Every peer
+// access touches the peer's own buffers (W.send / W.recv of that rank), so an in-place call whose
+// order were wrong would read overwritten data and fail the oracle comparison.
 bool read_step(World& W, Prog& P) {
   const int n = W.n, r = P.r, w = P.w;
   auto tx = [&](int d) { return W.tx_seq[r][(size_t)d * W.C + w]; };
   auto rx = [&](int q) { return W.rx_seq[r][(size_t)q * W.C + w]; };
   const uint64_t mpc = read_msgs_per_call(W.iters);
+  auto fold = [&](uint32_t it, bool push) {  // slice `it` of chunk r, stored (and pushed)
+    const uint64_t s = (uint64_t)it * W.A + w;
+    const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
+    const uint64_t coff = (uint64_t)r * W.chunk_bytes + s * W.slice;
+    const float* local = (const float*)((const char*)W.send[r] + coff);
+    std::vector<float> res((size_t)(len / 4));
+    for (uint64_t i = 0; i < len / 4; ++i) {
+      float acc = local[i];
+      for (int k = 1; k < n; ++k) {
+        const int q = direct_peer(n, r, k);
+        acc = apply(W.op, ((const float*)((const char*)W.send[q] + coff))[i], acc);
+      }
+      res[(size_t)i] = acc;
+    }
+    // every load of the slice came first (in place, recv chunk r of a peer is its send chunk r)
+    if (len) {
+      memcpy((char*)W.recv[r] + coff, res.data(), (size_t)len);
+      if (push)
+        for (int k = 1; k < n; ++k) memcpy((char*)W.recv[direct_peer(n, r, k)] + coff, res.data(), (size_t)len);
+    }
+  };
   switch (P.j) {
     case 0:
       for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx(direct_peer(n, r, k)) + 1;
@@ -197,31 +149,34 @@ bool read_step(World& W, Prog& P) {
       P.it = 0;
       P.k = 0;
       return true;
-    case 2: {
-      if (P.it < W.iters) {
-        const uint64_t s = (uint64_t)P.it * W.A + w;
-        const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
-        const uint64_t coff = (uint64_t)r * W.chunk_bytes + s * W.slice;
-        const float* local = (const float*)((const char*)W.send[r] + coff);
-        std::vector<float> res((size_t)(len / 4));
-        for (uint64_t i = 0; i < len / 4; ++i) {
-          float acc = local[i];
-          for (int k = 1; k < n; ++k) {
-            const int q = direct_peer(n, r, k);
-            acc = apply(W.op, ((const float*)((const char*)W.send[q] + coff))[i], acc);
-          }
-          res[(size_t)i] = acc;
-        }
-        // every load of the slice came first (in place, recv chunk r of a peer is its send chunk r)
-        if (len) {
-          memcpy((char*)W.recv[r] + coff, res.data(), (size_t)len);
-          for (int k = 1; k < n; ++k) memcpy((char*)W.recv[direct_peer(n, r, k)] + coff, res.data(), (size_t)len);
-        }
-        ++P.it;
+    case 2:
+      if (W.push) {
+        if (P.it < W.iters) fold(P.it++, true);
+        if (P.it >= W.iters) P.j = 3;
+        return true;
       }
-      if (P.it >= W.iters) P.j = 3;
+      if (P.k == 0) {
+        if (P.it < W.iters) {
+          fold(P.it, false);
+          for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx(direct_peer(n, r, k)) + 2 + P.it;
+        }
+        if (P.it > 0) P.k = 1;
+        else ++P.it;
+      } else {
+        const uint32_t t = P.it - 1;
+        const int q = direct_peer(n, r, 1 + (P.k - 1 + w) % (n - 1));
+        if (W.ready(r, q, w) < rx(q) + 2 + t) return false;
+        const uint64_t s = (uint64_t)t * W.A + w;
+        const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
+        const uint64_t coff = (uint64_t)q * W.chunk_bytes + s * W.slice;
+        memcpy((char*)W.recv[r] + coff, (const char*)W.recv[q] + coff, len);
+        if (++P.k == n) {
+          P.k = 0;
+          ++P.it;
+        }
+      }
+      if (P.it > W.iters) P.j = 3;
       return true;
-    }
     case 3:
       for (int k = 1; k < n; ++k) {
         const int q = direct_peer(n, r, k);
@@ -243,9 +198,6 @@ bool read_step(World& W, Prog& P) {
 extern "C" {
 
 // csrc/schedule.h effective_slice, exported for the host-logic tests
-void mnccl_direct_phase_at(uint32_t j, uint32_t iters, int overlap, int* phase, uint32_t* it) {
-  direct_phase_at(j, iters, overlap, phase, it);
-}
 uint64_t mnccl_effective_slice(uint64_t chunk_bytes, int channels, uint64_t slice, uint64_t min_slice, int depth) {
   return effective_slice(chunk_bytes, channels, slice, min_slice, depth);
 }
@@ -264,20 +216,23 @@ uint64_t mnccl_read_slice(uint64_t chunk_bytes, int channels, uint64_t slice, ui
   return read_slice(chunk_bytes, channels, slice, min_slice, depth);
 }
 
+int mnccl_call_pipelines(uint64_t nslices, int channels, int waves) { return call_pipelines(nslices, channels, waves); }
+
 // Runs `calls` consecutive all-reduces (send -> recv, fp32; send == recv for in place) on n
 // simulated ranks with the GPU kernels' protocol; call i uses schedule (algo >> 2i) & 3 (0 ring,
-// 1 direct, 2 read; schedules can alternate on one communicator state, as mncclCommSetAlgo
-// allows).  schedule_seed != 0 permutes the order programs are tried in
-// (pseudo-random), exploring different interleavings.  Returns 0, -1 on deadlock,
+// 2 read in its push form, 3 read in its load form; schedules can alternate on one communicator
+// state, as mncclCommSetAlgo allows).  schedule_seed != 0 permutes the order programs are tried
+// in (pseudo-random), exploring different interleavings.  min_slice: 0 = fixed payload (the
+// configured slice), else the adaptive payload of Comm::launch.  Returns 0, -1 on deadlock,
 // -2 on bad arguments.  *steps_out = ops executed.
 int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* recv, int n, uint64_t count, int op,
-                        uint64_t slice_bytes, uint64_t min_slice, int direct_overlap, int pull, int channels,
-                        int slots, int calls, uint64_t schedule_seed, uint64_t* steps_out) {
+                        uint64_t slice_bytes, uint64_t min_slice, int channels, int slots, int calls,
+                        uint64_t schedule_seed, uint64_t* steps_out) {
   if (n < 1 || n > 16 || channels < 1 || slots < 1 || slice_bytes < 4 || slice_bytes % 4) return -2;
+  for (int call = 0; call < calls; ++call)
+    if (((algo >> (2 * call)) & 3) == 1) return -2;  // the direct schedule is gone (4.0)
   World W;
-  W.n = n; W.C = channels; W.K = slots; W.op = op; W.algo = algo; W.slot_bytes = slice_bytes;
-  W.overlap = direct_overlap;
-  W.pull = pull;
+  W.n = n; W.C = channels; W.K = slots; W.op = op; W.algo = (int)algo; W.slot_bytes = slice_bytes;
   const uint64_t chunk = count / (uint64_t)n;
   W.chunk_bytes = chunk * 4;
   W.send.assign(send, send + n);
@@ -290,14 +245,16 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
   uint64_t steps = 0;
   uint64_t rng = schedule_seed * 6364136223846793005ull + 1442695040888963407ull;
   for (int call = 0; call < calls; ++call) {
-    const int a = (int)((algo >> (2 * call)) & 3);
+    const int code = (int)((algo >> (2 * call)) & 3);
+    const int a = code >= 2 ? 2 : 0;
+    W.push = code == 2;
     // as Comm::launch: adaptive payload (min_slice 0 = off; the read schedule's own rule), fixed
-    // slot stride
+    // slot stride, one pipeline per slice up to all of them
     if (!min_slice) W.slice = slice_bytes;
     else if (a == 2) W.slice = read_slice(W.chunk_bytes, channels, slice_bytes, min_slice, kReadDepth);
     else W.slice = effective_slice(W.chunk_bytes, channels, slice_bytes, min_slice, 1);
     W.nslices = (W.chunk_bytes + W.slice - 1) / W.slice;
-    W.A = a == 2 ? read_pipelines(W.nslices, channels, 1) : channels;  // as Comm::launch
+    W.A = call_pipelines(W.nslices, channels, 1);
     W.iters = (uint32_t)((W.nslices + (uint64_t)W.A - 1) / (uint64_t)W.A);
     for (int r = 0; r < n; ++r) {  // send -> recv copy of the tail (Comm::allreduce)
       if ((const void*)recv[r] == (const void*)send[r]) continue;  // in place
@@ -329,7 +286,7 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
           burst = 1 + (int)((rng >> 40) % 4);
         }
         for (int b = 0; b < burst && !P.done; ++b) {
-          const bool ok = a == 2 ? read_step(W, P) : a == 1 ? direct_step(W, P) : ring_step(W, P);
+          const bool ok = a == 2 ? read_step(W, P) : ring_step(W, P);
           if (!ok) break;
           any = true;
           ++steps;
@@ -339,7 +296,7 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
       if (all_done) break;
       if (!any) return -1;  // deadlock
     }
-    // the kernels' last action per channel: advance the per-pair FIFO counters
+    // the kernels' last action per pipeline that ran: advance the per-pair FIFO counters
     for (int r = 0; r < n; ++r)
       for (int w = 0; w < W.A; ++w) {
         if (a == 2) {
@@ -347,12 +304,6 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
             if (q == r) continue;
             W.tx_seq[r][(size_t)q * channels + w] += read_msgs_per_call(W.iters);
             W.rx_seq[r][(size_t)q * channels + w] += read_msgs_per_call(W.iters);
-          }
-        } else if (a == 1) {
-          for (int q = 0; q < n; ++q) {
-            if (q == r) continue;
-            W.tx_seq[r][(size_t)q * channels + w] += (uint64_t)W.iters * direct_msgs_per_iter();
-            W.rx_seq[r][(size_t)q * channels + w] += (uint64_t)W.iters * direct_msgs_per_iter();
           }
         } else {
           const uint64_t m = (uint64_t)W.iters * ring_msgs_per_iter(n);

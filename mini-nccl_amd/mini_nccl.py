@@ -35,8 +35,8 @@ ncclFloat16, ncclFloat, ncclDouble, ncclBfloat16 = 6, 7, 8, 9
 # ncclRedOp_t (reference :43-49)
 ncclSum, ncclProd, ncclMax, ncclMin, ncclAvg = 0, 1, 2, 3, 4
 
-# mncclAlgo_t
-ALGO_AUTO, ALGO_RING, ALGO_DIRECT, ALGO_READ = -1, 0, 1, 2
+# mncclAlgo_t (mncclAlgoDirect = 1 was removed in mncclVersion 400)
+ALGO_AUTO, ALGO_RING, ALGO_READ = -1, 0, 2
 
 DTYPE_SIZE = {ncclInt32: 4, ncclFloat16: 2, ncclFloat: 4, ncclDouble: 8, ncclBfloat16: 2}
 
@@ -54,6 +54,8 @@ class CommInfo(ctypes.Structure):
         # since mncclVersion 300
         ("ipc_open_failures", ctypes.c_ulonglong), ("read_map_failures", ctypes.c_ulonglong),
         ("read_rounds", ctypes.c_ulonglong), ("closed_freed", ctypes.c_ulonglong), ("live_exports", ctypes.c_size_t),
+        # since mncclVersion 400
+        ("cap_refusals", ctypes.c_ulonglong), ("liveness_queries", ctypes.c_ulonglong), ("read_push", ctypes.c_int),
     ]
 
 

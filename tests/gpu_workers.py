@@ -142,6 +142,92 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def many_buffers_rank(rank, n, port, env, pairs, out_q):
+    """`pairs` distinct send / recv allocations, all alive until the end (a data-parallel caller's
+    gradient buckets), one read call on each in turn: every call bit-exact; the process's export
+    cap (512) sends the calls beyond it to the ring on every rank, counted in cap_refusals; the
+    per-call liveness queries stay bounded (the call's own buffers + a batch of 4, ipcreg.h)."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        hip_rt.set_device(0)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        comm.set_algo(2)
+        st = hip_rt.Stream()
+        count = 4099
+        bufs = [(hip_rt.DeviceBuffer(count * 4, fresh=True), hip_rt.DeviceBuffer(count * 4, fresh=True))
+                for _ in range(pairs)]
+        bad, rcs, algos, queries = 0, [], [], []
+        for i, (s, r) in enumerate(bufs):
+            xs = make_inputs(n, count, "f32", 2000 + i, False)
+            s.upload(xs[rank])
+            q0 = comm.info()["liveness_queries"]
+            rc = comm.all_reduce(s.ptr, r.ptr, count, M.ncclFloat, M.ncclSum, st.handle)
+            st.sync()
+            ci = comm.info()
+            queries.append(ci["liveness_queries"] - q0)
+            rcs.append(rc)
+            algos.append(ci["last_algo"])
+            bad += compare(r.download(np.float32, count), O.allreduce(xs, "f32", "sum")[rank], "f32", True)[0]
+        # the same buffers again: all of them are known now (no mapping round), still exact
+        for i, (s, r) in enumerate(bufs[:64]):
+            xs = make_inputs(n, count, "f32", 5000 + i, False)
+            s.upload(xs[rank])
+            rcs.append(comm.all_reduce(s.ptr, r.ptr, count, M.ncclFloat, M.ncclSum, st.handle))
+            st.sync()
+            bad += compare(r.download(np.float32, count), O.allreduce(xs, "f32", "sum")[rank], "f32", True)[0]
+        info = comm.info()
+        for s, r in bufs:
+            s.free()
+            r.free()
+        st.destroy()
+        out_q.put((rank, {"bad": bad, "rcs": rcs, "algos": algos, "queries": queries, "info": info,
+                          "destroy": comm.destroy()}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
+def release_rank(rank, n, port, env, nbytes, out_q, barrier=None):
+    """memory a caller frees after its last communicator is destroyed must come back.
+    Every rank runs a read call on its own `nbytes` allocation (exported as a dma-buf, imported by
+    the peers), destroys the communicator, then the ranks free their allocations one at a time
+    and each measures the device's free memory around its own hipFree."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        hip_rt.set_device(0)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        comm.set_algo(2)
+        count = nbytes // 4
+        buf = hip_rt.DeviceBuffer(nbytes, fresh=True)
+        buf.upload(np.ones(count, np.float32))
+        hip_rt.sync()
+        rc = comm.all_reduce(buf.ptr, buf.ptr, count, M.ncclFloat, M.ncclSum, 0)
+        hip_rt.sync()
+        got = buf.download(np.float32, 1024)
+        info = comm.info()
+        rc_destroy = comm.destroy()
+        barrier.wait(120)  # every communicator is gone
+        freed = 0
+        for r in range(n):
+            if r == rank:
+                f0, _ = hip_rt.mem_get_info()
+                buf.free()
+                hip_rt.sync()
+                f1, _ = hip_rt.mem_get_info()
+                freed = f1 - f0
+            barrier.wait(120)
+        out_q.put((rank, {"rc": rc, "destroy": rc_destroy, "last_algo": info["last_algo"], "freed": freed,
+                          "ok": bool((got == n).all())}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
 def two_comms_rank(rank, n, ports, env, rounds, out_q):
     """Two communicators in one process sharing the same send / recv buffers, calls alternating
     between them; every other round on fresh allocations (freed after it).  Each communicator

@@ -42,6 +42,8 @@ def lib():
         _hip.hipGraphDestroy.argtypes = [vp]
         _hip.hipStreamWaitValue32.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint, ctypes.c_uint32]
         _hip.hipStreamWaitValue32.restype = i
+        _hip.hipMemGetInfo.argtypes = [ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        _hip.hipMemGetInfo.restype = i
         for f in ("hipStreamBeginCapture", "hipStreamEndCapture", "hipGraphInstantiate", "hipGraphLaunch",
                   "hipGraphExecDestroy", "hipGraphDestroy"):
             getattr(_hip, f).restype = i
@@ -66,6 +68,13 @@ def device_count():
 
 def set_device(d):
     check(lib().hipSetDevice(d), "hipSetDevice")
+
+
+def mem_get_info():
+    """(free, total) bytes of the current device (hipMemGetInfo)."""
+    f, t = ctypes.c_size_t(), ctypes.c_size_t()
+    check(lib().hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)), "hipMemGetInfo")
+    return f.value, t.value
 
 
 _cache = {}  # segment bytes -> free segments (device pointers) of that size

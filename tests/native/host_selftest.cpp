@@ -2,7 +2,7 @@
 // on host code only -- GPU ASan is not available on the test pool).  Built and run by
 // tests/test_host_sanitizers.py with g++ -fsanitize=address,undefined; exercises the code
 // the GPU path shares with the CPU simulator: csrc/schedule.h index math (through sim.cpp's
-// kernel-mirroring programs: ring, direct and read), the TCP bootstrap (threads over 127.0.0.1),
+// kernel-mirroring programs: the ring and both forms of read), the TCP bootstrap (threads over 127.0.0.1),
 // the read schedule's shared-memory call board (csrc/peerbuf.cpp) and env config parsing.
 #include <stdint.h>
 #include <stdio.h>
@@ -14,16 +14,16 @@
 
 extern "C" {
 int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* recv, int n, uint64_t count, int op,
-                        uint64_t slice_bytes, uint64_t min_slice, int direct_overlap, int pull, int channels,
-                        int slots, int calls, uint64_t schedule_seed, uint64_t* steps_out);
+                        uint64_t slice_bytes, uint64_t min_slice, int channels, int slots, int calls,
+                        uint64_t schedule_seed, uint64_t* steps_out);
 int mnccl_bootstrap_selftest(int rank, int nranks, const char* ip, int port, int timeout_ms);
 int mnccl_config_describe(char* buf, int len);
 int mnccl_board_selftest(int rank, int nranks, const char* ip, int port, int scenario, int calls, double timeout_s,
                          int* decisions);
 }
 
-static int sim_case(int algo, int n, uint64_t count, uint64_t slice, uint64_t min_slice, int overlap, int channels,
-                    int slots, int calls, uint64_t seed) {
+static int sim_case(int algo, int n, uint64_t count, uint64_t slice, uint64_t min_slice, int channels, int slots,
+                    int calls, uint64_t seed) {
   std::mt19937 g((unsigned)(seed * 7 + n));
   std::uniform_real_distribution<float> u(-1.f, 1.f);
   std::vector<std::vector<float>> s((size_t)n, std::vector<float>(count)), r((size_t)n, std::vector<float>(count));
@@ -38,9 +38,8 @@ static int sim_case(int algo, int n, uint64_t count, uint64_t slice, uint64_t mi
   uint64_t steps = 0;
   uint64_t mask = 0;  // 2 bits per call: the schedule of every call
   for (int c = 0; c < calls; ++c) mask |= (uint64_t)algo << (2 * c);
-  // pull placement on odd seeds: the same protocol with every slot in the sender's scratch
-  const int rc = mnccl_sim_allreduce(mask, sp.data(), rp.data(), n, count, 0, slice, min_slice, overlap, (int)(seed & 1),
-                                     channels, slots, calls, seed, &steps);
+  const int rc = mnccl_sim_allreduce(mask, sp.data(), rp.data(), n, count, 0, slice, min_slice, channels, slots, calls,
+                                     seed, &steps);
   if (rc != 0) return 1;
   // every rank holds the same bits in the body (the count % n tail keeps each rank's own
   // input; the oracle comparison lives in the Python tests)
@@ -54,13 +53,13 @@ static int sim_case(int algo, int n, uint64_t count, uint64_t slice, uint64_t mi
 int main() {
   int fails = 0;
   const uint64_t counts[] = {7, 1000, 4099, 70001};
-  for (int algo = 0; algo < 3; ++algo)
+  for (int algo : {0, 2, 3})  // ring, read (push form), read (load form)
     for (int n = 2; n <= 8; n += 3)
       for (uint64_t c : counts)
-        for (int overlap = 0; overlap < 2; ++overlap) {
-          const int rc = sim_case(algo, n, c, 256, overlap ? 64 : 0, overlap, 3, 2 + (int)(c % 2), 2, c + (uint64_t)n);
+        for (int adaptive = 0; adaptive < 2; ++adaptive) {
+          const int rc = sim_case(algo, n, c, 256, adaptive ? 64 : 0, 3, 2 + (int)(c % 2), 2, c + (uint64_t)n);
           if (rc) {
-            printf("sim FAIL algo=%d n=%d count=%llu overlap=%d rc=%d\n", algo, n, (unsigned long long)c, overlap, rc);
+            printf("sim FAIL algo=%d n=%d count=%llu adaptive=%d rc=%d\n", algo, n, (unsigned long long)c, adaptive, rc);
             ++fails;
           }
         }

@@ -18,13 +18,12 @@ def load():
     if _lib is None:
         L = ctypes.CDLL(LIB)
         vp, u64, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
-        L.mnccl_sim_allreduce.argtypes = [u64, ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64, u64, i, i, i, i, i,
+        L.mnccl_sim_allreduce.argtypes = [u64, ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64, u64, i, i, i,
                                           u64, ctypes.POINTER(u64)]
         L.mnccl_board_selftest.argtypes = [i, i, ctypes.c_char_p, i, i, i, ctypes.c_double, ctypes.POINTER(i)]
         L.mnccl_read_slice.argtypes = [u64, i, u64, u64, i]
         L.mnccl_read_slice.restype = u64
-        L.mnccl_direct_phase_at.argtypes = [ctypes.c_uint32, ctypes.c_uint32, i, ctypes.POINTER(i),
-                                            ctypes.POINTER(ctypes.c_uint32)]
+        L.mnccl_call_pipelines.argtypes = [u64, i, i]
         L.mnccl_effective_slice.argtypes = [u64, i, u64, u64, i]
         L.mnccl_effective_slice.restype = u64
         L.mnccl_bootstrap_selftest.argtypes = [i, i, ctypes.c_char_p, i, i]
@@ -34,13 +33,16 @@ def load():
     return _lib
 
 
+RING, READ, READ_LOAD = 0, 2, 3  # schedules: the ring, read in its push form, read in its load form
+
+
 def allreduce(inputs, algo=0, op=0, slice_bytes=1024, channels=4, slots=2, calls=1, seed=0, algos=None, min_slice=0,
-              direct_overlap=1, pull=0, inplace=False):
+              inplace=False):
     """fp32 all-reduce of `inputs` (one array per rank) through the simulated kernels,
-    `calls` times on one communicator state (schedule `algo` -- 0 ring, 1 direct, 2 read -- for
-    every call, or the per-call list `algos`; at most 32 calls).  inplace: send == recv (then
-    every call after the first reduces the previous result).  Returns (outputs, steps); raises
-    RuntimeError on deadlock."""
+    `calls` times on one communicator state (schedule `algo` -- RING, READ (push form) or
+    READ_LOAD (MINI_NCCL_READ_PUSH=0) -- for every call, or the per-call list `algos`; at most 32
+    calls).  inplace: send == recv (then every call after the first reduces the previous
+    result).  Returns (outputs, steps); raises RuntimeError on deadlock."""
     if algos is None:
         algos = [algo] * calls
     calls = len(algos)
@@ -52,10 +54,8 @@ def allreduce(inputs, algo=0, op=0, slice_bytes=1024, channels=4, slots=2, calls
     sp = (ctypes.c_void_p * n)(*[s.ctypes.data for s in sends])
     rp = (ctypes.c_void_p * n)(*[r.ctypes.data for r in recvs])
     steps = ctypes.c_uint64()
-    rc = load().mnccl_sim_allreduce(mask, sp, rp, n, sends[0].size, op, slice_bytes, min_slice, direct_overlap, pull,
-                                    channels, slots,
-                                    calls, seed,
-                                    ctypes.byref(steps))
+    rc = load().mnccl_sim_allreduce(mask, sp, rp, n, sends[0].size, op, slice_bytes, min_slice, channels, slots,
+                                    calls, seed, ctypes.byref(steps))
     if rc == -1:
         raise RuntimeError("simulated protocol deadlocked")
     if rc != 0:
@@ -85,10 +85,9 @@ def read_slice(chunk_bytes, channels, slice_bytes, min_slice, depth=16):
     return load().mnccl_read_slice(chunk_bytes, channels, slice_bytes, min_slice, depth)
 
 
-def direct_phase_at(j, iters, overlap):
-    ph, it = ctypes.c_int(), ctypes.c_uint32()
-    load().mnccl_direct_phase_at(j, iters, overlap, ctypes.byref(ph), ctypes.byref(it))
-    return ph.value, it.value
+def call_pipelines(nslices, channels, waves=1):
+    """csrc/schedule.h call_pipelines: the pipelines a call of `nslices` slices runs."""
+    return load().mnccl_call_pipelines(nslices, channels, waves)
 
 
 def board_selftest(rank, nranks, port, scenario, calls, timeout_s=2.0):

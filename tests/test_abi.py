@@ -93,7 +93,19 @@ def test_argument_checks_before_device_work(nccl_lib):
     assert L.mncclLocalReduce(fake, fake, fake, 4, M.ncclFloat, M.ncclAvg, None) == M.ncclInternalError
     assert L.mncclLocalReduce(None, fake, fake, 4, M.ncclFloat, M.ncclSum, None) == M.ncclInvalidArgument
     assert L.mncclCommSetAlgo(None, 0) == M.ncclInvalidArgument
-    assert L.mncclVersion() >= 100
+    assert L.mncclVersion() == 400
+
+
+def test_info_struct_layout(nccl_lib):
+    import mini_nccl as M
+    # mncclCommGetInfo (legacy) writes the pre-300 prefix only; mncclCommGetInfoV the whole struct
+    names = [f for f, _ in M.CommInfo._fields_]
+    assert names.index("ipc_open_failures") < names.index("cap_refusals") < names.index("read_push")
+    hdr = open(HEADERS[1]).read()
+    body = hdr[hdr.index("typedef struct {"):hdr.index("} mncclCommInfo_t;")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    hdr_fields = re.findall(r"(\w+)(?:\[\d+\])?\s*[,;]", body)
+    assert hdr_fields == names, (hdr_fields, names)
 
 
 def test_init_without_gpu_fails_cleanly(nccl_lib):
@@ -139,7 +151,7 @@ def test_config_from_env(sim_lib, monkeypatch):
     # reference defaults (Config.h:29-47): 128 KiB, 64, 16; workgroups derived per communicator
     # (channels=0, schedule.h pipeline_geometry); no auto-tune at init; 512 MiB scratch cap
     assert "SLICE_SIZE=131072 B" in s and "WINDOW=64" in s and "BATCH=16" in s and "channels=0" in s
-    assert "algo=auto" in s and "threads=64" in s and "sys_fence=0" in s and "min_slice=1024" in s
+    assert "algo=auto" in s and "threads=64" in s and "sys_fence=0" in s and "read_push=1" in s
     assert "scratch_cap=512 MiB" in s
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", "0")       # Config.h:50: 0 -> 1024
     monkeypatch.setenv("MINI_NCCL_WINDOW_SIZE", "-3")     # Config.h:51: <= 0 -> 1
@@ -149,10 +161,14 @@ def test_config_from_env(sim_lib, monkeypatch):
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", str(8 << 30))  # 32-bit message lengths: clamped
     rc, s = S.config_describe()
     assert rc == 0 and f"SLICE_SIZE={256 << 20} B" in s
-    monkeypatch.setenv("MINI_NCCL_ALGO", "direct")
+    monkeypatch.setenv("MINI_NCCL_ALGO", "ring")
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", "100")     # rounded down to whole 16-byte vectors
+    monkeypatch.setenv("MINI_NCCL_READ_PUSH", "0")        # the read schedule's load form
     rc, s = S.config_describe()
-    assert "algo=direct" in s and "SLICE_SIZE=96 B" in s
+    assert "algo=ring" in s and "SLICE_SIZE=96 B" in s and "read_push=0" in s
+    monkeypatch.setenv("MINI_NCCL_ALGO", "direct")        # removed in 4.0: an init error, not a silent ring
+    rc, s = S.config_describe()
+    assert rc == -1 and "no longer" in s
     monkeypatch.setenv("MINI_NCCL_ALGO", "auto")
     rc, s = S.config_describe()
     assert rc == 0 and "algo=auto" in s

@@ -2,10 +2,11 @@
 
 * mncclLocalReduce (the scatter-reduce element-wise kernel alone) vs oracle_reduce,
   every dtype x op, vector and scalar (misaligned / odd-size) paths, bit-exact;
-* ncclAllReduce with 2-4 rank processes sharing GPU 0 (as the reference's perf_test
-  does, tests/perf_test.cpp:46), ring and direct schedules, in/out of place, odd
-  counts (tail), repeated calls, slices smaller than a chunk, bit-exact vs the oracle
-  (NaN payloads of +/* excepted: NaN-ness must match);
+* ncclAllReduce with 2-10 rank processes sharing GPU 0 (as the reference's perf_test
+  does, tests/perf_test.cpp:46), the ring and the read schedule (push form, and its load
+  form MINI_NCCL_READ_PUSH=0 where the protocol differs), in/out of place, odd counts
+  (tail), repeated calls, slices smaller than a chunk, bit-exact vs the oracle (NaN
+  payloads of +/* excepted: NaN-ness must match);
 * error paths: watchdog timeout -> ncclInternalError and a sticky error afterwards.
 """
 import os
@@ -21,6 +22,10 @@ pytestmark = pytest.mark.gpu
 
 DTYPES = ["f32", "f64", "i32", "f16", "bf16"]
 OPS = ["sum", "prod", "max", "min"]
+LOAD_FORM = {"MINI_NCCL_READ_PUSH": "0"}
+# (schedule, extra environment): the ring, read (push form, the default), read's load form
+SCHEDULES = [pytest.param((0, {}), id="ring"), pytest.param((2, {}), id="read")]
+SCHEDULES_ALL = SCHEDULES + [pytest.param((2, LOAD_FORM), id="read_load")]
 
 
 @pytest.fixture(scope="module")
@@ -76,7 +81,7 @@ def _run_allreduce(n, cases, env=None, timeout=300, barrier=True):
             if c["algo"] == 2 and dev_bufs and c["count"] >= n:
                 assert res["last_algo"] == 2, f"rank {r} case {c}: ran schedule {res['last_algo']}"
             # no IPC open ever failed (nothing retries: a failure would send a call to the
-            # scratch schedule, csrc/peerbuf.cpp), in this process or in any rank's mapping round
+            # ring, csrc/peerbuf.cpp), in this process or in any rank's mapping round
             assert res["ipc_open_failures"] == 0 and res["read_map_failures"] == 0, (r, c, res)
     return out
 
@@ -87,9 +92,10 @@ def _case(dtype="f32", op="sum", count=1 << 18, inplace=False, algo=0, calls=1, 
                 offset=offset, **kw)
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
+@pytest.mark.parametrize("sched", SCHEDULES_ALL)
 @pytest.mark.parametrize("n", [2, 3, 4])
-def test_allreduce_fp32_sum(dev, n, algo):
+def test_allreduce_fp32_sum(dev, n, sched):
+    algo, env = sched
     cases = [
         _case(count=1 << 20, algo=algo),                     # 4 MiB: C1's size
         _case(count=(1 << 18) + 3, algo=algo, inplace=True),  # tail of count % n
@@ -97,16 +103,15 @@ def test_allreduce_fp32_sum(dev, n, algo):
         _case(count=n - 1, algo=algo),                       # count < n: copy only
         _case(count=123457, algo=algo, calls=3, seed=9),     # repeated calls, odd size
     ]
-    _run_allreduce(n, cases)
+    _run_allreduce(n, cases, env)
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
-@pytest.mark.parametrize("stage_host", ["0", "1"], ids=["mapped", "staged"])
-def test_host_buffers(dev, algo, stage_host):
+@pytest.mark.parametrize("algo", [0, 2], ids=["ring", "read"])
+def test_host_buffers(dev, algo):
     # the reference's perf_test hands cudaHostAlloc'd (pinned host) buffers straight to
     # ncclAllReduce (perf_test.cpp:78-79,88): pinned memory is read and written by the kernel
-    # through its device mapping (or staged with MINI_NCCL_STAGE_HOST=1), pageable memory is
-    # staged through HBM; mixed placements and ranks whose buffers differ must agree
+    # through its device mapping, pageable memory is staged through HBM; mixed placements and
+    # ranks whose buffers differ must agree (a read call with host buffers runs the ring)
     cases = [
         _case(count=(1 << 20) + 3, algo=algo, mem="pinned"),
         _case(count=(1 << 18) + 1, algo=algo, mem="pinned", inplace=True, seed=5),
@@ -117,25 +122,25 @@ def test_host_buffers(dev, algo, stage_host):
         _case(dtype="bf16", count=300001, algo=algo, mem="pinned", calls=2, seed=10),
         _case(count=(1 << 20) + 1, algo=algo, mem=("device", "pinned", "pageable"), seed=11),
     ]
-    _run_allreduce(3, cases, env={"MINI_NCCL_STAGE_HOST": stage_host})
+    _run_allreduce(3, cases)
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
+@pytest.mark.parametrize("sched", SCHEDULES_ALL)
 @pytest.mark.parametrize("blocking", ["1", "0"], ids=["blocking", "async"])
-def test_skewed_ranks_varying_data(dev, algo, blocking):
+def test_skewed_ranks_varying_data(dev, sched, blocking):
+    algo, env = sched
     # injected delays (SURVEY.md §5 race detection): every rank sleeps 0-30 ms before each of
     # 4 calls, inputs change every call and every call is checked; sizes alternate so the
     # adaptive payload changes between calls while a peer may still drain the previous one
     cases = [_case(count=c, algo=algo, calls=4, seed=40 + i, vary=True, skew_ms=30)
              for i, c in enumerate(((1 << 20) + 3, 5000, (1 << 18) + 1))]
     cases += [_case(dtype="bf16", count=300007, algo=algo, calls=4, seed=50, vary=True, skew_ms=30, inplace=True)]
-    _run_allreduce(4, cases, env={"MINI_NCCL_BLOCKING": blocking})
+    _run_allreduce(4, cases, env={"MINI_NCCL_BLOCKING": blocking, **env})
 
 
-def test_auto_schedule_from_devices_no_init_allreduce(dev):
-    # MINI_NCCL_ALGO=auto (default): the read schedule, with a scratch fallback that comes from
-    # the gathered device records (every rank on one GPU -> ring at any n); no all-reduce runs
-    # at init
+def test_auto_schedule_no_init_allreduce(dev):
+    # MINI_NCCL_ALGO=auto (default): the read schedule (push form), the ring as its fallback; no
+    # all-reduce runs at init
     port = GW.free_port()
     out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {}), 120)
     assert all("error" not in out[r] for r in range(3)), out
@@ -143,36 +148,22 @@ def test_auto_schedule_from_devices_no_init_allreduce(dev):
         i = out[r]["info"]
         # auto = the read schedule; its fallback for buffers that cannot be shared: the ring here
         assert i["tune_ms"] == [0.0, 0.0] and i["algo"] == 2 and i["scratch_algo"] == 0, i
+        assert i["read_push"] == 1 and i["calib_choice"] == -1 and i["calib_ms"] == [0.0, 0.0], i
         assert i["ranks_on_device"] == 3 and i["last_algo"] == -1, i
         assert i["channels"] == 256 and i["pipelines"] == 256 and i["slot_bytes"] == 128 << 10
         assert i["scratch_bytes"] == 2 * 256 * 2 * (128 << 10)  # (n-1) peer regions
     port = GW.free_port()
-    out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {"MINI_NCCL_ALGO": "direct"}), 120)
-    assert out[0]["info"]["tune_ms"] == [0.0, 0.0] and out[0]["info"]["algo"] == 1
+    out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {"MINI_NCCL_ALGO": "ring", **LOAD_FORM}), 120)
+    assert out[0]["info"]["algo"] == 0 and out[0]["info"]["read_push"] == 0
+    # MINI_NCCL_ALGO=direct (removed in 4.0) fails init instead of silently running another schedule
+    import mini_nccl as M
+    port = GW.free_port()
+    out = GW.run_ranks(GW.init_rank, 2, lambda r: (r, 2, port, {0: {"MINI_NCCL_ALGO": "direct"},
+                                                               1: {"MINI_NCCL_ALGO": "direct"}}), 120)
+    assert out[0]["rc"] == M.ncclSystemError and out[1]["rc"] == M.ncclSystemError
 
 
-def test_measured_choice_between_read_and_scratch(dev):
-    # MINI_NCCL_CALIBRATE (on by default when the ranks span several GPUs; forced here on the one
-    # GPU): large auto calls 0-3 run read and the scratch schedule to warm up, then the scratch
-    # schedule and read timed; every rank publishes its timings with its call records, all decide
-    # alike on the first call where every rank's are in, and later large calls run the faster --
-    # every call bit-exact vs the oracle
-    n = 3
-    cases = [_case(count=1 << 20, algo=-1, seed=300 + i) for i in range(7)]
-    env = {"MINI_NCCL_CALIBRATE": "1", "MINI_NCCL_CALIBRATE_BYTES": str(1 << 20)}
-    out = _run_allreduce(n, cases, env)
-    seqs = [[res["last_algo"] for res in out[r]["results"]] for r in range(n)]
-    assert all(s == seqs[0] for s in seqs), seqs
-    choice = out[0]["info"]["calib_choice"]
-    assert choice in (0, 2), out[0]["info"]  # read, or this one-GPU communicator's scratch (ring)
-    assert seqs[0][:4] == [2, 0, 0, 2] and seqs[0][4:] == [choice] * 3, seqs[0]
-    for r in range(n):
-        i = out[r]["info"]
-        assert i["calib_choice"] == choice and i["calib_ms"][0] > 0 and i["calib_ms"][1] > 0, i
-        assert i["calib_ms"] == out[0]["info"]["calib_ms"]  # max over ranks: the same on every rank
-
-
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
+@pytest.mark.parametrize("algo", [0, 2], ids=["ring", "read"])
 def test_sys_fence_on(dev, algo):
     # MINI_NCCL_SYS_FENCE=1: system release / acquire fences around every hand-off (the
     # default relies on sc0 sc1 payload accesses of uncached scratch instead)
@@ -180,8 +171,9 @@ def test_sys_fence_on(dev, algo):
     _run_allreduce(3, cases, env={"MINI_NCCL_SYS_FENCE": "1"})
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
-def test_allreduce_8_ranks(dev, algo):
+@pytest.mark.parametrize("sched", SCHEDULES_ALL)
+def test_allreduce_8_ranks(dev, sched):
+    algo, env = sched
     # the 8-GPU node's rank count, all on GPU 0 at the library's default geometry (256
     # pipelines): every pair of the mesh exercised; BASELINE C3 (fp32) and C5 (fp16, bf16) on
     # order-sensitive seeded data, bit-exact vs the oracle
@@ -189,10 +181,10 @@ def test_allreduce_8_ranks(dev, algo):
              _case(dtype="f16", count=(1 << 20) + 3, algo=algo, inplace=True, seed=9),  # C5 fp16
              _case(dtype="bf16", count=(1 << 19) + 3, algo=algo, inplace=True, seed=10),  # C5 bf16
              _case(count=8 * 4099 + 7, algo=algo, calls=2, seed=11)]
-    _run_allreduce(8, cases, timeout=600)
+    _run_allreduce(8, cases, env, timeout=600)
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
+@pytest.mark.parametrize("algo", [0, 2], ids=["ring", "read"])
 def test_allreduce_10_ranks(dev, algo):
     # past a node's 8 ranks (up to 16 per communicator): the read kernel's one-peer-ahead fold and
     # its peer groups of 7 in the short-slice forms; 10 rank processes on the one GPU with 64
@@ -222,7 +214,7 @@ def test_allreduce_8_ranks_c3_ring_128mib(dev):
     _run_allreduce(8, cases, timeout=600)
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
+@pytest.mark.parametrize("algo", [0, 2], ids=["ring", "read"])
 @pytest.mark.parametrize("n", [2, 4])
 @pytest.mark.parametrize("slice_kib", [64, 256, 1024])
 def test_allreduce_slice_points(dev, slice_kib, n, algo):
@@ -236,11 +228,12 @@ def test_allreduce_slice_points(dev, slice_kib, n, algo):
     _run_allreduce(n, cases, env={"MINI_NCCL_SLICE_SIZE": str(sl), "MINI_NCCL_CHANNELS": "16"}, timeout=600)
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
-def test_allreduce_dtypes_ops(dev, algo):
+@pytest.mark.parametrize("sched", SCHEDULES_ALL)
+def test_allreduce_dtypes_ops(dev, sched):
+    algo, env = sched
     cases = [_case(dtype=d, op=o, count=50000 + 7 * i, algo=algo, seed=100 + i, special=o in ("max", "min"))
              for i, (d, o) in enumerate((d, o) for d in DTYPES for o in OPS)]
-    _run_allreduce(3, cases)
+    _run_allreduce(3, cases, env)
 
 
 def test_read_schedule_count_mismatch_is_invalid_usage(dev):
@@ -373,24 +366,24 @@ def test_allreduce_c2_full_size(dev):
 
 def test_allreduce_small_slices_many_messages(dev):
     # 1 KiB slices, 4 channels: thousands of flag hand-offs per call, both schedules
-    cases = [_case(count=(1 << 19) + 5, algo=a, calls=2, seed=77) for a in (0, 1, 2)]
+    cases = [_case(count=(1 << 19) + 5, algo=a, calls=2, seed=77) for a in (0, 2)]
     _run_allreduce(4, cases, env={"MINI_NCCL_SLICE_SIZE": "1024", "MINI_NCCL_CHANNELS": "4"})
 
 
 def test_allreduce_misaligned_buffers(dev):
     # dword-aligned but not 16-byte-aligned buffers (vector path with straddling vectors)
     # and 2-byte-aligned halves with odd chunks (element path)
-    cases = [_case(count=40001, algo=a, offset=o, seed=5) for a in (0, 1, 2) for o in (4, 8, 12)]
-    cases += [_case(dtype="bf16", count=30001, algo=a, offset=2, seed=6) for a in (0, 1, 2)]
+    cases = [_case(count=40001, algo=a, offset=o, seed=5) for a in (0, 2) for o in (4, 8, 12)]
+    cases += [_case(dtype="bf16", count=30001, algo=a, offset=2, seed=6) for a in (0, 2)]
     _run_allreduce(3, cases)
 
 
 def test_allreduce_async_mode(dev):
-    cases = [_case(count=1 << 20, algo=a, calls=4, seed=3) for a in (0, 1, 2)]
+    cases = [_case(count=1 << 20, algo=a, calls=4, seed=3) for a in (0, 2)]
     _run_allreduce(2, cases, env={"MINI_NCCL_BLOCKING": "0"})
 
 
-@pytest.mark.parametrize("algo", ["ring", "direct", "read"])
+@pytest.mark.parametrize("algo", ["ring", "read"])
 def test_destroy_waits_for_calls_in_flight(dev, algo):
     port = GW.free_port()
     env = {"MINI_NCCL_BLOCKING": "0", "MINI_NCCL_ALGO": algo, "MINI_NCCL_TIMEOUT_MS": "30000"}
@@ -434,7 +427,7 @@ def test_late_peer_is_aborted_fast(dev, algo):
     assert out[1]["secs"] < 1.5, out[1]  # well under its own 1.5 s watchdog + 2 s host limit
 
 
-@pytest.mark.parametrize("algo", ["ring", "direct", "read"])
+@pytest.mark.parametrize("algo", ["ring", "read"])
 def test_allreduce_hip_graph_capture_and_replay(dev, algo):
     # the reference only warns under capture (api.cpp:153-166); here a captured all-reduce
     # replays correctly because the FIFO counters are device state advanced by the kernel
@@ -448,10 +441,10 @@ def test_allreduce_hip_graph_capture_and_replay(dev, algo):
         assert out[r]["bad"] == [0, 0, 0, 0]
         assert out[r]["eager_rc"] == 0 and out[r]["eager_bad"] == 0
         # the read schedule is captured too (its peer mappings pinned for the replays)
-        assert out[r]["captured_algo"] == {"ring": 0, "direct": 1, "read": 2}[algo]
+        assert out[r]["captured_algo"] == {"ring": 0, "read": 2}[algo]
 
 
-@pytest.mark.parametrize("algo", ["ring", "direct", "read"])
+@pytest.mark.parametrize("algo", ["ring", "read"])
 def test_calls_on_alternating_streams_are_ordered(dev, algo):
     port = GW.free_port()
     env = {"MINI_NCCL_TIMEOUT_MS": "20000", "MINI_NCCL_ALGO": algo, "MINI_NCCL_BLOCKING": "0"}
@@ -481,8 +474,8 @@ def test_single_rank_is_copy_only(dev):
     _run_allreduce(1, cases)
 
 
-@pytest.mark.parametrize("knob,values", [("MINI_NCCL_SLICE_SIZE", ("131072", "65536")), ("MINI_NCCL_PULL", ("0", "1")),
-                                         ("MINI_NCCL_ALGO", ("ring", "direct")), ("MINI_NCCL_CALIBRATE", ("0", "1")),
+@pytest.mark.parametrize("knob,values", [("MINI_NCCL_SLICE_SIZE", ("131072", "65536")),
+                                         ("MINI_NCCL_READ_PUSH", ("1", "0")), ("MINI_NCCL_ALGO", ("ring", "read")),
                                          ("MINI_NCCL_WINDOW_SIZE", ("64", "16"))])
 def test_mismatched_config_is_system_error(dev, knob, values):
     # every init failure is ncclSystemError, as in the reference (api.cpp:62-65)
@@ -514,16 +507,52 @@ def test_watchdog_deadline_starts_with_the_kernel(dev):
         assert out[r]["secs"] >= 5.5 and out[r]["destroy"] == 0, out[r]
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
-@pytest.mark.parametrize("n", [2, 3])
-def test_pull_placement(dev, algo, n):
-    # MINI_NCCL_PULL=1: every slot in the sender's scratch, loaded by the receiver over the link
-    # (the comparison form for xGMI, csrc/schedule.h); same flags and credits, same bits
-    cases = [_case(count=(1 << 20) + 3, algo=algo, seed=31),
-             _case(dtype="bf16", op="max", count=77777, algo=algo, seed=32, special=True),
-             _case(dtype="f64", count=50001, algo=algo, inplace=True, calls=2, seed=33),
-             _case(dtype="i32", op="prod", count=4099, algo=algo, seed=34)]
-    _run_allreduce(n, cases, env={"MINI_NCCL_PULL": "1"})
+@pytest.mark.parametrize("n", [2, 8])
+def test_ring_small_calls_run_only_their_pipelines(dev, n):
+    # the ring launches one pipeline per slice up to all 256 (schedule.h call_pipelines): calls
+    # from 1 slice to the full grid, interleaved with read calls on the same communicator (its
+    # idle pipelines' counters must stay in step on every rank), bit-exact vs the oracle
+    sizes = [n * 64 + 1, 1000, n * 1024 * 7 + 3, 4099, n * 256 * 1024 + 5, 77, (1 << 20) + 3]
+    cases = [_case(count=c, algo=(0 if i % 3 else 2), seed=1700 + i, vary=True, calls=2, inplace=i % 2 == 1)
+             for i, c in enumerate(sizes)]
+    _run_allreduce(n, cases, {"GPU_MAX_HW_QUEUES": "2"}, timeout=300)
+
+
+def test_read_schedule_many_live_buffers(dev):
+    # ~600 distinct live allocations per rank (300 send / recv pairs), one read call
+    # each: bit-exact; past the process's 512-export cap the calls run the ring on every rank
+    # alike, counted (cap_refusals) and warned once; the pointer queries per call stay bounded by
+    # the call's own buffers + a batch of 4, whatever the number of live exports
+    n, pairs = 2, 300
+    port = GW.free_port()
+    out = GW.run_ranks(GW.many_buffers_rank, n, lambda r: (r, n, port, {"MINI_NCCL_TIMEOUT_MS": "30000"}, pairs), 600)
+    assert sorted(out) == list(range(n)), out
+    for r in range(n):
+        o = out[r]
+        assert "error" not in o, o["error"]
+        assert o["bad"] == 0 and all(rc == 0 for rc in o["rcs"]) and o["destroy"] == 0, o["bad"]
+        assert o["algos"][:256] == [2] * 256, o["algos"][:256]  # 512 exports: 256 pairs share
+        assert all(a == 0 for a in o["algos"][256:]), o["algos"][256:]  # beyond the cap: the ring
+        assert o["info"]["cap_refusals"] > 0 and o["info"]["live_exports"] == 512, o["info"]
+        assert max(o["queries"]) <= 2 + 4, o["queries"]
+        assert o["info"]["ipc_open_failures"] == 0 and o["info"]["read_map_failures"] == 0, o["info"]
+    assert out[0]["algos"] == out[1]["algos"]
+
+
+def test_destroy_releases_shared_memory(dev):
+    # an allocation a read call exported (dma-buf) and the peers imported is released
+    # by its owner's hipFree once every communicator is destroyed (destroy closes the imports of
+    # peers no live communicator talks to, and the last one closes the process's exports)
+    n, nbytes = 3, 256 << 20
+    port = GW.free_port()
+    out = GW.run_ranks(GW.release_rank, n, lambda r: (r, n, port, {"MINI_NCCL_TIMEOUT_MS": "30000"}, nbytes), 300,
+                       barrier=True)
+    assert sorted(out) == list(range(n)), out
+    for r in range(n):
+        o = out[r]
+        assert "error" not in o, o["error"]
+        assert o["rc"] == 0 and o["destroy"] == 0 and o["ok"] and o["last_algo"] == 2, o
+        assert o["freed"] >= nbytes * 9 // 10, o  # the memory came back at hipFree
 
 
 def test_count_beyond_int32(dev):

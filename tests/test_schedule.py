@@ -20,7 +20,7 @@ def same_bits(a, b):
     return np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
+@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_LOAD], ids=["ring", "read", "read_load"])
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
 @pytest.mark.parametrize("count,slice_bytes,channels,slots", [
     (4096, 256, 4, 2),      # several slices per channel
@@ -37,7 +37,7 @@ def test_sim_matches_oracle(oracle_lib, sim_lib, algo, n, count, slice_bytes, ch
         assert same_bits(got[r], ref[r]), f"rank {r}"
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
+@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_LOAD], ids=["ring", "read", "read_load"])
 @pytest.mark.parametrize("op", OPS)
 def test_sim_all_ops(oracle_lib, sim_lib, algo, op):
     xs = O.random_inputs(4, 2050, "f32", seed=11)
@@ -46,7 +46,7 @@ def test_sim_all_ops(oracle_lib, sim_lib, algo, op):
     assert all(same_bits(g, e) for g, e in zip(got, ref))
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
+@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_LOAD], ids=["ring", "read", "read_load"])
 @pytest.mark.parametrize("seed", range(1, 13))
 def test_sim_random_interleavings_no_deadlock(oracle_lib, sim_lib, algo, seed):
     n = 2 + seed % 7
@@ -57,7 +57,7 @@ def test_sim_random_interleavings_no_deadlock(oracle_lib, sim_lib, algo, seed):
     assert all(same_bits(g, e) for g, e in zip(got, ref))
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
+@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_LOAD], ids=["ring", "read", "read_load"])
 def test_sim_sequence_continues_across_calls(oracle_lib, sim_lib, algo):
     # 5 calls on one communicator state: flags are monotone and never reset
     xs = O.random_inputs(4, 5000, "f32", seed=5)
@@ -69,24 +69,26 @@ def test_sim_sequence_continues_across_calls(oracle_lib, sim_lib, algo):
 
 
 def test_ring_message_counts(sim_lib):
-    # per channel iteration: 2n-1 ops for the ring (1 send + (n-1) SR + (n-1) AG receives)
+    # per pipeline iteration: 2n-1 ops for the ring (1 send + (n-1) SR + (n-1) AG receives); a
+    # call runs only the pipelines its slices need (schedule.h call_pipelines): 1 slice -> 1
     n, C = 4, 2
     xs = O.random_inputs(n, n * 16, "f32")
-    _, steps = S.allreduce(xs, algo=0, slice_bytes=64, channels=C, slots=2)
-    iters = -(-(16 * 4 // 64) // C)  # ceil(nslices / C), nslices = 1
-    assert steps == n * C * iters * (2 * n - 1)
+    _, steps = S.allreduce(xs, algo=S.RING, slice_bytes=64, channels=C, slots=2)
+    assert steps == n * 1 * 1 * (2 * n - 1)  # nslices = 1: one pipeline, one iteration
+    xs = O.random_inputs(n, n * 16 * 5, "f32")  # 5 slices over 2 pipelines: 3 iterations
+    _, steps = S.allreduce(xs, algo=S.RING, slice_bytes=64, channels=C, slots=2)
+    assert steps == n * C * 3 * (2 * n - 1)
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
-def test_single_slot_fifo_deadlocks(sim_lib, algo):
-    # why Config clamps MINI_NCCL_SLOTS to >= 2: with one slot per channel, op k of every
+def test_single_slot_fifo_deadlocks(sim_lib):
+    # why Config clamps MINI_NCCL_SLOTS to >= 2: with one slot per pipeline, op k of every
     # rank waits for the credit its neighbour only returns inside ITS op k -- a cycle
     xs = O.random_inputs(2, 4096, "f32")
     with pytest.raises(RuntimeError, match="deadlock"):
-        S.allreduce(xs, algo=algo, slice_bytes=256, channels=2, slots=1)
+        S.allreduce(xs, algo=S.RING, slice_bytes=256, channels=2, slots=1)
 
 
-@pytest.mark.parametrize("algos", [[0, 1, 0, 1], [1, 1, 0, 0, 1], [0, 0, 1], [2, 0, 2, 1, 2], [1, 2, 2, 0]])
+@pytest.mark.parametrize("algos", [[0, 2, 0, 2], [3, 3, 0, 0, 2], [0, 0, 3], [2, 0, 2, 3, 2], [3, 2, 2, 0]])
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
 def test_sim_switching_schedules_on_one_communicator(oracle_lib, sim_lib, algos, n):
     # mncclCommSetAlgo between calls: per-pair FIFO counters keep every link consistent
@@ -114,7 +116,7 @@ def test_effective_slice_properties(sim_lib, chunk, C):
     assert S.effective_slice(chunk, C, slice_bytes, slice_bytes) == slice_bytes  # MIN_SLICE >= SLICE: off
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2], ids=["ring", "direct", "read"])
+@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_LOAD], ids=["ring", "read", "read_load"])
 @pytest.mark.parametrize("n,count,seed", [(2, 70001, 1), (3, 40000, 2), (4, 9000, 3), (8, 123457, 4)])
 def test_sim_adaptive_slice(oracle_lib, sim_lib, algo, n, count, seed):
     # payload shrunk below the slot stride, random interleavings over 3 calls: same bits
@@ -124,44 +126,39 @@ def test_sim_adaptive_slice(oracle_lib, sim_lib, algo, n, count, seed):
     assert all(same_bits(g, e) for g, e in zip(got, ref))
 
 
-@pytest.mark.parametrize("overlap", [0, 1], ids=["plain", "overlapped"])
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
 @pytest.mark.parametrize("seed", range(1, 9))
-def test_sim_direct_phase_orders(oracle_lib, sim_lib, overlap, seed):
-    # both direct phase orders (csrc/schedule.h direct_phase_at) under random interleavings,
-    # several iterations per pipeline, 2 and 3 slots: same bits, no deadlock
-    n = 2 + seed % 7
-    xs = O.random_inputs(n, 5000 + 13 * seed, "f32", seed=seed)
-    ref = O.allreduce(xs, slice_bytes=64)
-    got, _ = S.allreduce(xs, algo=1, slice_bytes=64, channels=1 + seed % 3, slots=2 + seed % 2, calls=2,
-                         seed=seed, direct_overlap=overlap)
-    assert all(same_bits(g, e) for g, e in zip(got, ref))
+def test_sim_ring_partial_grid_random_interleavings(oracle_lib, sim_lib, n, seed):
+    # the ring runs only the pipelines a call's slices need (schedule.h call_pipelines; the
+    # reference moves only the slices that exist, mini_nccl.cu:112-115): calls of 1 .. C slices
+    # interleaved with full-grid calls and read calls on one communicator state, random
+    # interleavings -- the idle pipelines' per-pair counters stay in step on every rank
+    C = 8
+    sizes = [n * 16, n * 16 * 3 + 1, n * 16 * C * 2 + 5, n * 16 * 5 + 3, 7, n * 16 * C + 16]
+    for i, count in enumerate(sizes):
+        xs = O.random_inputs(n, count, "f32", seed=100 * seed + i)
+        ref = O.allreduce(xs, slice_bytes=64)
+        algos = [S.RING, S.RING, S.READ if i % 2 else S.READ_LOAD, S.RING]
+        got, _ = S.allreduce(xs, slice_bytes=64, channels=C, slots=2, algos=algos, seed=seed + i)
+        assert all(same_bits(g, e) for g, e in zip(got, ref)), (count, algos)
 
 
-def test_direct_phase_order_is_a_permutation(sim_lib):
-    # every (phase, iteration) exactly once, A(t) before B(t) before C(t), A(t+1) before C(t)
-    for iters in (1, 2, 3, 7):
-        for overlap in (0, 1):
-            seen = [S.direct_phase_at(j, iters, overlap) for j in range(3 * iters)]
-            assert sorted(seen) == sorted((ph, t) for t in range(iters) for ph in range(3))
-            pos = {x: i for i, x in enumerate(seen)}
-            for t in range(iters):
-                assert pos[(0, t)] < pos[(1, t)] < pos[(2, t)]
-                if overlap and t + 1 < iters:
-                    assert pos[(0, t + 1)] < pos[(2, t)]
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_ring_small_calls_run_only_the_pipelines_they_need(oracle_lib, sim_lib, n):
+    # a 3-slice ring call on 8 pipelines executes 3 pipelines' ops, not 8
+    C, count = 8, n * 48
+    xs = O.random_inputs(n, count, "f32", seed=60 + n)
+    got, steps = S.allreduce(xs, algo=S.RING, slice_bytes=64, channels=C)
+    assert steps == n * 3 * (2 * n - 1)
+    assert all(same_bits(g, e) for g, e in zip(got, O.allreduce(xs, slice_bytes=64)))
 
 
-@pytest.mark.parametrize("algo", [0, 1], ids=["ring", "direct"])
-@pytest.mark.parametrize("seed", range(1, 9))
-def test_sim_pull_placement(oracle_lib, sim_lib, algo, seed):
-    # MINI_NCCL_PULL=1 (csrc/schedule.h slot_owner / slot_region): every slot lives in the
-    # sender's scratch and the receiver loads it; same flags and credits, so the same bits and
-    # no deadlock under random interleavings, with several calls and iterations per pipeline
-    n = 2 + seed % 7
-    xs = O.random_inputs(n, 4000 + 17 * seed, "f32", seed=seed)
-    ref = O.allreduce(xs, slice_bytes=64)
-    got, _ = S.allreduce(xs, algo=algo, slice_bytes=64, channels=1 + seed % 3, slots=2 + seed % 2, calls=3,
-                         seed=seed, pull=1)
-    assert all(same_bits(g, e) for g, e in zip(got, ref))
+@pytest.mark.parametrize("nslices,C,waves,want", [(0, 256, 1, 1), (1, 256, 1, 1), (3, 8, 1, 3), (255, 256, 1, 255),
+                                                  (256, 256, 1, 256), (10**6, 256, 1, 256), (3, 64, 4, 4),
+                                                  (5, 64, 4, 8), (70, 64, 4, 64)])
+def test_call_pipelines(sim_lib, nslices, C, waves, want):
+    # one pipeline per slice up to all C, whole workgroups of `waves` pipelines
+    assert S.call_pipelines(nslices, C, waves) == want
 
 
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
@@ -172,25 +169,29 @@ def test_sim_read_in_place_random_interleavings(oracle_lib, sim_lib, n, seed):
     # interleavings any earlier write would leave a wrong value behind
     xs = O.random_inputs(n, 3000 + 7 * seed, "f32", seed=seed)
     ref = O.allreduce(xs, slice_bytes=64)
-    got, _ = S.allreduce(xs, algo=2, slice_bytes=64, channels=1 + seed % 4, calls=1, seed=seed, inplace=True)
-    assert all(same_bits(g, e) for g, e in zip(got, ref))
+    for algo in (S.READ, S.READ_LOAD):
+        got, _ = S.allreduce(xs, algo=algo, slice_bytes=64, channels=1 + seed % 4, calls=1, seed=seed, inplace=True)
+        assert all(same_bits(g, e) for g, e in zip(got, ref)), algo
 
 
 def test_sim_read_needs_no_slots(oracle_lib, sim_lib):
-    # no scratch FIFO: even one slot (which deadlocks the scratch schedules) is irrelevant
+    # no scratch FIFO: even one slot (which deadlocks the ring) is irrelevant
     xs = O.random_inputs(3, 4096, "f32", seed=3)
-    got, _ = S.allreduce(xs, algo=2, slice_bytes=256, channels=2, slots=1)
+    got, _ = S.allreduce(xs, algo=S.READ, slice_bytes=256, channels=2, slots=1)
     assert all(same_bits(g, e) for g, e in zip(got, O.allreduce(xs, slice_bytes=256)))
 
 
 def test_read_message_counts(sim_lib):
     # per pipeline and call: START (publish + wait), one fold-and-push per iteration (push form:
-    # no READY, no copies), DONE (publish + wait)
+    # no READY, no copies), DONE (publish + wait); load form: per iteration one fold (+ READY)
+    # and n-1 copies, one extra step to leave the loop
     n, C = 4, 2
     xs = O.random_inputs(n, n * 64, "f32")
-    _, steps = S.allreduce(xs, algo=2, slice_bytes=64, channels=C)
+    _, steps = S.allreduce(xs, algo=S.READ, slice_bytes=64, channels=C)
     iters = -(-(64 * 4 // 64) // C)
     assert steps == n * C * (4 + iters)
+    _, steps = S.allreduce(xs, algo=S.READ_LOAD, slice_bytes=64, channels=C)
+    assert steps == n * C * (4 + iters * n + 1)
 
 
 @pytest.mark.parametrize("chunk", [0, 4, 1000, 1 << 16, (1 << 20) + 12, 3 << 22, 1 << 27, 1 << 30])
@@ -211,14 +212,14 @@ def test_read_slice_properties(sim_lib, chunk, C):
 
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
 def test_read_small_calls_run_only_the_pipelines_they_need(oracle_lib, sim_lib, n):
-    # schedule.h read_pipelines: a read call with fewer slices than pipelines runs one pipeline per
+    # schedule.h call_pipelines: a read call with fewer slices than pipelines runs one pipeline per
     # slice; the rest sit it out on every rank, so their per-pair counters stay in step through
-    # later calls of any schedule (ring and direct run every pipeline, idle ones included)
+    # later calls of either schedule
     C, count = 8, n * 48  # 192 B chunks of 64 B slices: 3 slices, 3 of the 8 pipelines
     xs = O.random_inputs(n, count, "f32", seed=40 + n)
     ref = O.allreduce(xs, slice_bytes=64)
     _, steps = S.allreduce(xs, algo=2, slice_bytes=64, channels=C)
     assert steps == n * 3 * (4 + 1)  # iters = 1 on 3 pipelines
     for seed in range(3):
-        got, _ = S.allreduce(xs, slice_bytes=64, channels=C, algos=[2, 0, 2, 1, 2, 2, 0, 1, 2], seed=seed + 1)
+        got, _ = S.allreduce(xs, slice_bytes=64, channels=C, algos=[2, 0, 2, 3, 2, 2, 0, 3, 2], seed=seed + 1)
         assert all(same_bits(g, e) for g, e in zip(got, ref))

@@ -88,6 +88,7 @@ def main():
             "read_bytes_per_launch": int(round(f_b)),
             "write_bytes_per_launch": int(round(w_b)),
             "algorithmic_bytes_per_launch": alg,
+            "kernel_form": "local_reduce",
             "traffic_over_algorithmic": round((f_b + w_b) / alg, 4),
             "dispatches": [len(fetch), len(write)],
             "source": f"profiles/{rnd}_n1_pmc.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "

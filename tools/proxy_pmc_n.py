@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""PMC passes of tools/r2_investigate.sh (gpurun_out/<tag>/{fetch,write}_<algo>_n<N>) -> per-launch
-HBM bytes of rank 0's ring / direct kernel on the N-rank one-GPU proxy, with the gfx950
-corrections (FETCH x2, KiB x1024, MI355X_MICROARCH.md), against the fused algorithmic bytes
-4 B x chunk x (6n - 4) (Kernels), next to the kernel-trace durations.
+"""PMC passes of tools/r2_investigate.sh (gpurun_out/<tag>/{fetch,write}_<form>_n<N>) -> per-launch
+HBM bytes of rank 0's kernel on the N-rank one-GPU proxy, with the gfx950 corrections (FETCH x2,
+KiB x1024, MI355X_MICROARCH.md), against the fused algorithmic bytes of its kernel form (bench.py
+fused_bytes: ring (6n-4) chunks, read_push 2n, read_load 3n-1), next to the kernel-trace durations.
 
-  python tools/proxy_pmc_n.py <tag> <round> <n> ring direct ...
+  python tools/proxy_pmc_n.py <tag> <round> <n> ring read_push read_load ...
       -> profiles/<round>_proxy_pmc_n<N>.csv, profiles/<round>_proxy_kernel_stats_n<N>.csv,
-         and the "<algo>_f32_1GiB_n<N>_same_gpu" entries of profiles/pmc_summary.json
+         and the "<form>_f32_1GiB_n<N>_same_gpu" entries of profiles/pmc_summary.json, each
+         carrying its kernel_form (bench.py refuses an entry of another form)
 """
 import csv
 import json
@@ -36,10 +37,10 @@ def med_after5(vals):
 
 def main():
     tag, rnd, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    algos = sys.argv[4:] or ["ring", "direct"]
+    algos = sys.argv[4:] or ["ring", "read_push"]
     base = os.path.join(ROOT, "gpurun_out", tag)
-    def fused_of(algo):  # bench.py fused_bytes: read has no scratch
-        return 4 * (COUNT // n) * ((2 * n) if algo == "read" else (6 * n - 4))
+    def fused_of(form):  # bench.py fused_bytes
+        return 4 * (COUNT // n) * {"ring": 6 * n - 4, "read_push": 2 * n, "read_load": 3 * n - 1}[form]
     summ_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     summ = json.load(open(summ_path)) if os.path.exists(summ_path) else {}
     pmc_csv = os.path.join(ROOT, "profiles", f"{rnd}_proxy_pmc_n{n}.csv")
@@ -51,7 +52,9 @@ def main():
                      "fused_alg_bytes", "fused_GBps_one_rank", "ranks_x_fused_GBps"])
         for algo in algos:
             fused = fused_of(algo)
-            k = f"{algo}_kernel"
+            # the kernel's template arguments name its form: read_kernel<float, 0, true, PUSH>
+            k = {"ring": "ring_kernel<float, 0, true>", "read_push": "read_kernel<float, 0, true, true>",
+                 "read_load": "read_kernel<float, 0, true, false>"}[algo]
             tr = rows(os.path.join(base, f"trace_{algo}_n{n}", "run_kernel_trace.csv"), k)
             durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr]
             md = med_after5(durs)
@@ -64,7 +67,7 @@ def main():
             rd = med_after5([float(r["Counter_Value"]) for r in fe]) * 1024 * 2
             wb = med_after5([float(r["Counter_Value"]) for r in wr]) * 1024
             summ[f"{algo}_f32_1GiB_n{n}_same_gpu"] = {
-                "kernel": tr[0]["Kernel_Name"],
+                "kernel": tr[0]["Kernel_Name"], "kernel_form": algo,
                 "read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wb),
                 "hbm_bytes_per_launch": int(rd + wb), "fused_algorithmic_bytes_per_launch": fused,
                 "traffic_over_fused_algorithmic": round((rd + wb) / fused, 4),
@@ -72,7 +75,7 @@ def main():
                 "dispatches": [len(fe), len(wr)],
                 "note": f"{n} ranks sharing ONE MI355X (proxy); rank 0 profiled (apps/bin/perf_test --sizes 1024, "
                         "default knobs); medians after the first 5 dispatches; fused bytes = 4 B x chunk x (6n-4) for "
-                        "ring / direct, x 2n for read (push form)",
+                        "the ring, x 2n for read's push form, x (3n-1) for its load form",
                 "source": f"profiles/{rnd}_proxy_pmc_n{n}.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate "
                           "passes; FETCH x2, KiB x1024)",
             }
