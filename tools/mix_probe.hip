@@ -45,6 +45,71 @@ __global__ void __launch_bounds__(64) mix2(Streams s, unsigned long long nvec) {
 
 static const char* g_case = nullptr;
 
+// The read kernel's structure without its protocol (read_fold_all at n = 2: one peer stream and
+// the local stream read, the result stored twice, V vectors per lane per batch, the next batch's
+// loads issued before this one is stored): P persistent one-wave workgroups; BLOCKED = each wave
+// walks its own contiguous 1/P of the streams (as a read pipeline walks its own slices), else the
+// waves take batches round robin (batch k*P + w: all waves inside one window of memory).
+template <int V, bool BLOCKED>
+__global__ void __launch_bounds__(64) persist(Streams s, unsigned long long nvec) {
+  const int lane = threadIdx.x, w = blockIdx.x, P = gridDim.x;
+  const unsigned long long B = 64ull * V, nb = nvec / B, per = nb / P;
+  auto rs = [&](const void* p) { return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000); };
+  const auto r0 = rs(s.src[0]), r1 = rs(s.src[1]), w0 = rs(s.dst[0]), w1 = rs(s.dst[1]);
+  auto bidx = [&](unsigned long long k) { return BLOCKED ? per * w + k : k * P + w; };
+  v4u xa[V], ya[V], xb[V], yb[V];
+  auto load = [&](v4u(&x)[V], v4u(&y)[V], unsigned long long k) {
+    const unsigned base = (unsigned)(bidx(k) * B * 16);
+#pragma unroll
+    for (int u = 0; u < V; ++u) x[u] = __builtin_amdgcn_raw_buffer_load_b128(r1, base + (u * 64 + lane) * 16, 0, 17);
+#pragma unroll
+    for (int u = 0; u < V; ++u) y[u] = __builtin_amdgcn_raw_buffer_load_b128(r0, base + (u * 64 + lane) * 16, 0, 2);
+  };
+  auto store = [&](v4u(&x)[V], v4u(&y)[V], unsigned long long k) {
+    const unsigned base = (unsigned)(bidx(k) * B * 16);
+#pragma unroll
+    for (int u = 0; u < V; ++u) y[u] += x[u];
+#pragma unroll
+    for (int u = 0; u < V; ++u) __builtin_amdgcn_raw_buffer_store_b128(y[u], w0, base + (u * 64 + lane) * 16, 0, 17);
+#pragma unroll
+    for (int u = 0; u < V; ++u) __builtin_amdgcn_raw_buffer_store_b128(y[u], w1, base + (u * 64 + lane) * 16, 0, 17);
+  };
+  if (per == 0) return;
+  load(xa, ya, 0);
+  for (unsigned long long k = 0;;) {
+    if (k + 1 < per) load(xb, yb, k + 1);
+    store(xa, ya, k);
+    if (++k >= per) break;
+    if (k + 1 < per) load(xa, ya, k + 1);
+    store(xb, yb, k);
+    if (++k >= per) break;
+  }
+}
+
+template <int V, bool BLOCKED>
+void run_persist(Streams s, unsigned long long nvec, int P) {
+  if (g_case && strcmp(g_case, BLOCKED ? "pb" : "pi")) return;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((persist<V, BLOCKED>), dim3(P), dim3(64), 0, 0, s, nvec);
+  CK(hipEventRecord(e0, 0));
+  const int it = 20;
+  for (int i = 0; i < it; ++i) hipLaunchKernelGGL((persist<V, BLOCKED>), dim3(P), dim3(64), 0, 0, s, nvec);
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const unsigned long long done = nvec / (64ull * V) / P * P * 64ull * V;  // whole batches per wave
+  const double bytes = (double)done * 16 * 4;
+  printf("persistent %s, %d waves, V=%d, 2R:2W (read kernel at n = 2): %.3f ms per launch, %.0f GB/s = %.1f %% of 8 TB/s\n",
+         BLOCKED ? "blocked (each wave its own 1/P)" : "interleaved (batch k*P + w)", P, V, ms / it,
+         bytes / (ms / it * 1e-3) / 1e9, bytes / (ms / it * 1e-3) / 8e12 * 100);
+  fflush(stdout);
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+}
+
 template <int R, int W, int AUX>
 void run(Streams s, unsigned long long nvec, const char* form) {
   if (g_case) {
@@ -98,6 +163,12 @@ int main(int argc, char** argv) {
     run<4, 4, 17>(s, nvec, "sc0 sc1");
     run<3, 1, 2>(s, nvec, "nt");
     run<1, 2, 17>(s, nvec, "sc0 sc1");
+    for (int P : {512, 1024, 2048}) {
+      run_persist<12, true>(s, nvec, P);
+      run_persist<12, false>(s, nvec, P);
+    }
+    run_persist<4, true>(s, nvec, 2048);
+    run_persist<4, false>(s, nvec, 2048);
   }
   return 0;
 }

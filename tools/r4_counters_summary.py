@@ -83,6 +83,10 @@ def main():
             der["wait_inst_any_frac"] = g("SQ_WAIT_INST_ANY") / g("SQ_WAVE_CYCLES")
         if g("SQ_WAVE_CYCLES") and g("SQ_ACTIVE_INST_VMEM") is not None:
             der["active_vmem_frac"] = g("SQ_ACTIVE_INST_VMEM") / g("SQ_WAVE_CYCLES")
+        for kind in ("RD", "WR"):  # requests the L2 sent to DRAM vs all its memory-side requests (MALL hits)
+            dr, rq = g(f"TCC_EA0_{kind}REQ_DRAM_sum"), g(f"TCC_EA0_{kind}REQ_sum")
+            if dr is not None and rq:
+                der[f"ea_{kind.lower()}_dram_fraction"] = dr / rq
         if g("FETCH_SIZE") is not None:
             der["fetch_bytes"] = g("FETCH_SIZE") * 1024 * 2  # KiB; gfx950 FETCH x2 (MI355X_MICROARCH.md)
         if g("WRITE_SIZE") is not None:

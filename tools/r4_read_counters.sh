@@ -21,6 +21,7 @@ PASSES=(
   "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum GRBM_GUI_ACTIVE"
   "FETCH_SIZE GRBM_GUI_ACTIVE"
   "WRITE_SIZE GRBM_GUI_ACTIVE"
+  "TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum GRBM_GUI_ACTIVE"
 )
 run() {  # run <n> <algo> <pass-index>; algo "mix": tools/bin/mix_probe's R=2 W=2 sc0 sc1 stream alone
   local n=$1 algo=$2 k=$3
@@ -42,7 +43,7 @@ run() {  # run <n> <algo> <pass-index>; algo "mix": tools/bin/mix_probe's R=2 W=
   return $rc
 }
 for cfg in ${CFGS:-2:read 4:read 2:ring 1:mix}; do
-  for k in $(seq 0 $((${#PASSES[@]} - 1))); do
+  for k in ${PASS_SEL:-$(seq 0 $((${#PASSES[@]} - 1)))}; do
     run ${cfg%%:*} ${cfg#*:} $k || exit 10
   done
 done

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Small-call time at 2 / 4 / 8 rank processes sharing one GPU, ring and read (push form) and the
+# read schedule's load form (perf_test rank 0, 200 blocking calls per size): the round-4 library.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+export GPU_MAX_HW_QUEUES=2 MINI_NCCL_PERF_DEVICE=0
+for nr in ${NRS:-2 4 8}; do
+  for cfg in ring:1 read:1 read:0; do
+    algo=${cfg%%:*}; push=${cfg#*:}
+    port=$((21000 + RANDOM % 20000))
+    pids=()
+    for ((r = 1; r < nr; r++)); do
+      MINI_NCCL_ALGO=$algo MINI_NCCL_READ_PUSH=$push MINI_NCCL_PORT=$port timeout -k 5 120 $R/apps/bin/perf_test $r $nr \
+        --sizes 4k,64k,1 --iters 200 > /tmp/sc_$r.log 2>&1 &
+      pids+=($!)
+    done
+    MINI_NCCL_ALGO=$algo MINI_NCCL_READ_PUSH=$push MINI_NCCL_PORT=$port timeout -k 5 120 $R/apps/bin/perf_test 0 $nr \
+      --sizes 4k,64k,1 --iters 200 > /tmp/sc_0.log 2>&1
+    rc=$?
+    for p in "${pids[@]}"; do wait $p; done
+    echo "== n=$nr algo=$algo read_push=$push rc=$rc"
+    grep -E "^ +[0-9]+ " /tmp/sc_0.log
+    [ $rc -ne 0 ] && exit 9
+  done
+done
+exit 0
