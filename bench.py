@@ -722,11 +722,12 @@ def main():
     else:
         comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
         info = comm.info()
-        # the headline runs the library's default for device buffers (MINI_NCCL_ALGO=auto: the
-        # read schedule in its push form); --algo forces one schedule
+        # the headline runs the library's default for device buffers (MINI_NCCL_ALGO=auto: at the
+        # bench's sizes the read schedule in its push form -- one-shot is for calls of <= 64 KiB);
+        # --algo forces one schedule
         auto_mode = args.algo == "auto"
         if auto_mode:
-            args.algo = ALGO_NAMES[info["algo"]]
+            args.algo = "read" if info["algo"] < 0 else ALGO_NAMES[info["algo"]]
         headline_algo = args.algo
         send = torch.ones(count, device=dev, dtype=tdt)
         recv = torch.empty(count, device=dev, dtype=tdt)

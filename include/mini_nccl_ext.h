@@ -30,13 +30,14 @@ extern "C" {
    300 mncclCommInfo_t grew (mncclCommGetInfoV); 301 user buffers shared as dma-bufs,
    MINI_NCCL_TUNE removed; 400 the direct schedule and MINI_NCCL_PULL / DIRECT_OVERLAP /
    CALIBRATE / PIPE_DEPTH / MIN_SLICE / STAGE_HOST removed, MINI_NCCL_READ_PUSH added, the ring
-   runs only the pipelines a call's slices need, mncclCommInfo_t grew again (same prefix) */
-#define MNCCL_VERSION 400
+   runs only the pipelines a call's slices need, mncclCommInfo_t grew again (same prefix);
+   401 the one-shot schedule (mncclAlgoOneShot, auto for small calls) */
+#define MNCCL_VERSION 401
 
 /* schedules; all produce bit-identical results (same fold order per element) */
 typedef enum {
-  mncclAlgoAuto = -1,  /* the library's default: read for device buffers every rank can share,
-                          the ring for every other call */
+  mncclAlgoAuto = -1,  /* the library's default: one-shot for calls of at most 64 KiB, read for
+                          device buffers every rank can share, the ring for every other call */
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
   mncclAlgoDirect = 1, /* removed in 400 (never faster than the ring); mncclCommSetAlgo and
                           MINI_NCCL_ALGO reject it */
@@ -49,7 +50,13 @@ typedef enum {
                           after the call.  Load form (MINI_NCCL_READ_PUSH=0): every peer loads
                           the result from rank c's recv.  A call whose buffers some rank
                           cannot share (host memory, a full export table) runs the ring
-                          instead, on every rank alike */
+                          instead, on every rank alike */,
+  mncclAlgoOneShot = 3 /* since 401, small calls: every rank stores its whole input into every
+                          peer's scratch in one message per pipeline and folds all n chunks
+                          itself in the same order -- one hand-off instead of the ring's
+                          2(n-1).  mncclAlgoAuto takes it for calls of at most 64 KiB; forced,
+                          every call whose slices fit one scratch slot per pipeline (the others
+                          run as with mncclAlgoAuto) */
 } mncclAlgo_t;
 
 typedef struct {

@@ -195,7 +195,8 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
 ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo) {
   if (!comm) return ncclInvalidArgument;
   // mncclAlgoDirect (1) was removed in 400: it never beat the ring on any measured setup
-  if (algo != mncclAlgoRing && algo != mncclAlgoRead && algo != mncclAlgoAuto) return ncclInvalidArgument;
+  if (algo != mncclAlgoRing && algo != mncclAlgoRead && algo != mncclAlgoOneShot && algo != mncclAlgoAuto)
+    return ncclInvalidArgument;
   reinterpret_cast<Comm*>(comm)->set_algo(algo);
   return ncclSuccess;
 }

@@ -111,7 +111,7 @@ Comm::Comm(int nranks, int rank, const std::string& ip) : rank_(rank), nranks_(n
   cfg_ = Config::from_env();
   // auto: the read schedule (same bits; no scratch; each call falls back to the ring when some
   // rank's buffers cannot be shared)
-  algo_ = cfg_.algo >= 0 ? cfg_.algo : 2;
+  set_algo(cfg_.algo);
   if (nranks > kMaxRanks) throw std::invalid_argument("nRanks > 16 is not supported on one node");
   geo_ = pipeline_geometry(nranks, cfg_.channels, cfg_.threads, cfg_.window_size, cfg_.signal_batch, cfg_.slots,
                            cfg_.slice_size, cfg_.scratch_cap);
@@ -457,11 +457,13 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.chunk_bytes = chunk_bytes;
   const int C = wave_channels();
   p.slot_bytes = wave_slice();
-  p.slice_bytes = algo == 2 ? read_slice(chunk_bytes, C, cfg_.slice_size, kMinSlice, kReadDepth)
-                            : effective_slice(chunk_bytes, C, wave_slice(), kMinSlice, 1);
+  p.slice_bytes = algo == 2   ? read_slice(chunk_bytes, C, cfg_.slice_size, kMinSlice, kReadDepth)
+                  : algo == 3 ? oneshot_slice(chunk_bytes, n, C, wave_slice())
+                              : effective_slice(chunk_bytes, C, wave_slice(), kMinSlice, 1);
   p.nslices = (chunk_bytes + p.slice_bytes - 1) / p.slice_bytes;
-  // either kernel runs one pipeline per slice up to C (schedule.h call_pipelines)
-  const int A = call_pipelines(p.nslices, C, geo_.waves);
+  // every kernel runs one pipeline per slice up to C (schedule.h call_pipelines); the one-shot one
+  // per slice of every chunk
+  const int A = call_pipelines(algo == 3 ? p.nslices * (uint64_t)n : p.nslices, C, geo_.waves);
   p.iters = (uint32_t)((p.nslices + (uint64_t)A - 1) / (uint64_t)A);
   p.pipes = C;
   p.n = n;
@@ -486,8 +488,9 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.read_push = cfg_.read_push;
   p.tail_bytes = tail_bytes;
   const int nt = cfg_.threads, wg = A / geo_.waves;
-  hipError_t e = algo == 2 ? launch_read(dtype, op, vec, wg, nt, p, stream)
-                           : launch_ring(dtype, op, vec, wg, nt, p, stream);
+  hipError_t e = algo == 2   ? launch_read(dtype, op, vec, wg, nt, p, stream)
+                 : algo == 3 ? launch_oneshot(dtype, op, vec, wg, nt, p, stream)
+                             : launch_ring(dtype, op, vec, wg, nt, p, stream);
   hip_check(e, "kernel launch");
   last_algo_ = algo;
 }
@@ -539,7 +542,11 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     // buffers the read schedule already shares (live exports of this process, checked by reap())
     // need no pointer query: device memory of this GPU
     bool local_s = false, local_r = false;
-    const bool read_sched = algo_ == 2 && pbuf_.available();
+    // one-shot for small calls (auto) or wherever a call fits it (forced); then the read schedule
+    // where every rank can share its buffers, the ring otherwise -- a pure function of the call's
+    // size and the rank-uniform config up to the read rendezvous, which all ranks decide alike
+    const bool oneshot = (auto_ || algo_ == 3) && oneshot_fits(chunk_bytes, n, wave_channels(), wave_slice(), !auto_);
+    const bool read_sched = !oneshot && (algo_ == 2 || algo_ == 3) && pbuf_.available();
     if (read_sched) pbuf_.reap(send, recv);
     const Reach rs = read_sched && pbuf_.known(send) ? (local_s = true, Reach::kDevice) : reach(send, &ksend, &local_s);
     const Reach rr = read_sched && pbuf_.known(recv) ? (local_r = true, Reach::kDevice)
@@ -566,10 +573,10 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     // straddle 16-byte boundaries on the local side; each message's last len % 16 bytes go
     // element by element); element-wise path otherwise (2-byte types with odd chunks)
     bool vec = (((uintptr_t)ksend | (uintptr_t)krecv) % 4 == 0) && (chunk_bytes % 4 == 0);
-    int algo = 0;  // the ring unless every rank can share its buffers
+    int algo = oneshot ? 3 : 0;  // else the ring unless every rank can share its buffers
     const char* psend[kMaxRanks] = {};
     const char* precv[kMaxRanks] = {};
-    if (algo_ == 2 && pbuf_.available()) {
+    if (read_sched) {
       // the read schedule: every rank takes part in the rendezvous, all decide alike (a captured
       // call reads through mappings its replays keep using: imports stay open until their owner
       // frees the allocation, which invalidates the graph anyway)

@@ -32,9 +32,13 @@ class Comm {
   int nranks() const { return nranks_; }
   int device() const { return device_; }
   const Config& config() const { return cfg_; }
-  int algo() const { return algo_; }
-  // a < 0: the default (read for buffers every rank can share, the ring for the other calls)
-  void set_algo(int a) { algo_ = a < 0 ? 2 : a; }
+  int algo() const { return auto_ ? -1 : algo_; }
+  // a < 0: the default (one-shot for small calls, read for buffers every rank can share, the
+  // ring for the other calls); 0 ring, 2 read, 3 one-shot wherever a call fits it
+  void set_algo(int a) {
+    auto_ = a < 0;
+    algo_ = a < 0 ? 2 : a;
+  }
   int last_algo() const { return last_algo_; }  // schedule of the last launched kernel, -1: none
   size_t peer_mappings() const { return pbuf_.mapped_allocations(); }
   const PeerBuffers& peer_buffers() const { return pbuf_; }
@@ -60,7 +64,7 @@ class Comm {
   enum class Reach { kDevice, kMapped, kStaged };
   Reach reach(const void* p, const void** kernel_ptr, bool* local) const;
   void ensure_stage(size_t bytes, hipStream_t stream);
-  // algo: 0 ring, 2 read (psend / precv: every rank's buffers mapped here)
+  // algo: 0 ring, 2 read (psend / precv: every rank's buffers mapped here), 3 one-shot
   void launch(int algo, const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
               uint32_t seq, bool vec, const char* const* psend = nullptr, const char* const* precv = nullptr,
               size_t tail_bytes = 0);
@@ -75,7 +79,8 @@ class Comm {
   Config cfg_;
   Geometry geo_;
   int algo_ = 0;                 // 0 ring, 2 read (its calls fall back to the ring when some rank's
-                                 // buffers cannot be shared)
+                                 // buffers cannot be shared), 3 one-shot (larger calls: as auto)
+  bool auto_ = true;             // the default: small calls one-shot, the others as algo_ = 2
   int last_algo_ = -1;
   int ranks_on_device_ = 1;
   uint32_t call_seq_ = 0;        // kernel launches of this communicator (the kernel's start word)

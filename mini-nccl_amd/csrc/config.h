@@ -17,7 +17,7 @@ struct Config {
   int channels = 0;                // MINI_NCCL_CHANNELS workgroups (0 -> derived, Comm::geometry)
   size_t scratch_cap = 512u << 20; // MINI_NCCL_SCRATCH_MB cap on this rank's uncached scratch
   int threads = 64;                // MINI_NCCL_THREADS threads per workgroup (one pipeline per wave)
-  int algo = -1;                   // MINI_NCCL_ALGO    auto (-1) | ring (0) | read (2)
+  int algo = -1;                   // MINI_NCCL_ALGO    auto (-1) | ring (0) | read (2) | oneshot (3)
   int blocking = 1;                // MINI_NCCL_BLOCKING host waits for the stream (reference behaviour)
   int sys_fence = 0;               // MINI_NCCL_SYS_FENCE 1: system release / acquire fences around each hand-off
   int read_push = 1;               // MINI_NCCL_READ_PUSH read schedule: 1 = each rank pushes its result slices

@@ -48,6 +48,8 @@ hipError_t launch_ring(int dtype, int op, bool vec, int channels, int threads,
                        const CollParams& p, hipStream_t stream);
 hipError_t launch_read(int dtype, int op, bool vec, int channels, int threads,
                        const CollParams& p, hipStream_t stream);
+hipError_t launch_oneshot(int dtype, int op, bool vec, int channels, int threads,
+                          const CollParams& p, hipStream_t stream);
 // out[i] = op(local[i], incoming[i]) for i < count
 hipError_t launch_local_reduce(int dtype, int op, void* out, const void* local,
                                const void* incoming, uint64_t count, hipStream_t stream);

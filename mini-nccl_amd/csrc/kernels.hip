@@ -255,6 +255,16 @@ __device__ __forceinline__ bool wave_wait_ge(const u64* flag, u64 target, const 
   return __builtin_amdgcn_readfirstlane(ok) != 0;
 }
 
+// Lane l waits for its own word (the peers' READY / CREDIT / DONE words, one lane per peer):
+// every peer's flag is polled in the same round instead of one peer after the other (n - 1
+// uncached round trips in a row at every hand-off of the read and one-shot kernels).  True when
+// every active lane's word arrived; a lane that gives up sets the status as wait_ge does.
+__device__ __forceinline__ bool wave_wait_peers(const u64* flag, u64 target, bool active, const Ctl& c) {
+  int bad = 0;
+  if (active) bad = wait_ge(flag, target, c) ? 0 : 1;
+  return __builtin_amdgcn_ballot_w64(bad != 0) == 0;
+}
+
 // ---------------------------------------------------------------- message bodies (one wave)
 enum : int { kHasLocal = 1, kHasIn = 2, kWritesRecv = 4, kSends = 8, kReduces = 16 };
 template <int KIND> struct KindBits;
@@ -579,6 +589,9 @@ __device__ __forceinline__ void read_copy_wide(const CollParams& p, uint64_t sof
 #ifndef MNCCL_READ_FOLD_ALL
 #define MNCCL_READ_FOLD_ALL 1
 #endif
+#ifndef MNCCL_READ_V2
+#define MNCCL_READ_V2 12  // vectors per lane per batch at 2 ranks (fp16 / bf16: 2/3 of it)
+#endif
 #ifndef MNCCL_FOLD_ALL_MIN_N
 #define MNCCL_FOLD_ALL_MIN_N 2
 #endif
@@ -595,9 +608,16 @@ __device__ __forceinline__ void read_copy_wide(const CollParams& p, uint64_t sof
 // (profiles/r3_read_push_ab.txt).  PUSH = false is the load form (READY per iteration, then every
 // peer's result slice loaded over the links), kept as the comparison form.
 
+template <typename T, bool VEC>
+__device__ __forceinline__ void read_push_rest(const CollParams& p, uint64_t coff, uint32_t nbytes, uint32_t off0,
+                                               int lane);
+
+// Batches b0, b0 + step, b0 + 2 step, ... (vector indices) below nvec: the slice form walks one
+// slice (b0 = 0, step = one batch); the stream form (MNCCL_READ_STREAM) walks the whole chunk with
+// the pipelines interleaved batch by batch (b0 = w batches, step = A batches).
 template <typename T, int OPC, int G, int V, bool PUSH>
-__device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff, uint32_t nvec, int lane) {
-  constexpr uint32_t S = 64 * V;
+__device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff, uint32_t nvec, int lane,
+                                              uint32_t b0 = 0, uint32_t step = 64 * V) {
   const int n = p.n, r = p.rank, w = wave_id().w;
   const uint32_t vb = nvec * 16;
   const rsrc_t loc = make_rsrc(p.send + coff, vb), out = make_rsrc(p.recv + coff, vb);
@@ -641,16 +661,57 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
         }
     }
   };
-  uint32_t b = 0;
-  load(xa, aa, 0);
+  // The next batch's loads are issued unconditionally: past the slice they fall outside the
+  // buffer resources' range, return 0 and touch no memory.  A conditional prefetch made hipcc
+  // wait vmcnt(0) where the two paths join -- for the prefetch itself and, as loads and stores
+  // share vmcnt, for every store of the batch before: the double buffer then never overlapped
+  // (tools/mix_probe.hip "persist2"; profiles/r4_vmcnt.txt).  A slice is at most kMaxSlice, so
+  // the past-the-end offsets stay below 2^32; in the stream form (a chunk below 4 GiB) one that
+  // wraps lands inside the same buffer: a wasted load whose registers are never read.
+  uint32_t b = b0;
+  if (b >= nvec) return;
+  load(xa, aa, b);
   for (;;) {
-    if (b + S < nvec) load(xb, ab, b + S);
+    load(xb, ab, b + step);
     fold_store(xa, aa, b);
-    if ((b += S) >= nvec) break;
-    if (b + S < nvec) load(xa, aa, b + S);
+    if ((b += step) >= nvec) break;
+    load(xa, aa, b + step);
     fold_store(xb, ab, b);
-    if ((b += S) >= nvec) break;
+    if ((b += step) >= nvec) break;
   }
+}
+
+// The push form's whole chunk r in one stream (MNCCL_READ_STREAM): the push form has no
+// per-iteration message, so its slices are only a way to deal work; here pipeline w takes
+// batches w, w + A, w + 2A, ... of the chunk (the A pipelines sweep one window of memory
+// together) with the next batch's loads in flight across what used to be slice boundaries.
+// False: the chunk is too large for one buffer resource (the caller runs the slice form).
+#ifndef MNCCL_READ_STREAM
+#define MNCCL_READ_STREAM 0
+#endif
+template <typename T, int OPC>
+__device__ __forceinline__ bool read_push_stream(const CollParams& p, int w, int A, int lane) {
+  if (p.chunk_bytes >= (1ull << 32) - 64) return false;
+  const int n = p.n;
+  const uint64_t coff = (uint64_t)p.rank * p.chunk_bytes;
+  const uint32_t nvec = (uint32_t)(p.chunk_bytes >> 4);
+  constexpr int h = sizeof(T) == 2 ? 1 : 0;
+#define STREAM(G, V) read_fold_all<T, OPC, G, V, true>(p, coff, nvec, lane, (uint32_t)w * 64u * (V), (uint32_t)A * 64u * (V))
+  if (nvec) {
+    if (n == 2) STREAM(1, MNCCL_READ_V2 - (MNCCL_READ_V2 / 3) * h);
+    else if (n == 3) STREAM(2, 8 - 2 * h);
+    else if (n <= 5) STREAM(4, 4 - h);
+    else STREAM(7, 3 - h);
+  }
+#undef STREAM
+  // the chunk's last chunk_bytes % 16 bytes: pipeline 0, element by element, then pushed
+  const uint32_t tail0 = nvec * 16u, cb = (uint32_t)p.chunk_bytes;
+  if (w == 0 && cb > tail0) {
+    read_fold_scalar<T, OPC>(p, coff, cb, lane, tail0);
+    drain_stores();
+    read_push_rest<T, true>(p, coff, cb, tail0, lane);
+  }
+  return true;
 }
 
 // Returns the leading bytes of the slice whose result it also pushed to the peers (PUSH).
@@ -667,7 +728,7 @@ __device__ __forceinline__ uint32_t read_fold(const CollParams& p, uint64_t coff
     // variants within 256 registers without spilling)
     constexpr int h = sizeof(T) == 2 ? 1 : 0;
     if (!nvec) {
-    } else if (n == 2) read_fold_all<T, OPC, 1, 12 - 4 * h, PUSH>(p, coff, nvec, lane);
+    } else if (n == 2) read_fold_all<T, OPC, 1, MNCCL_READ_V2 - (MNCCL_READ_V2 / 3) * h, PUSH>(p, coff, nvec, lane);
     else if (n == 3) read_fold_all<T, OPC, 2, 8 - 2 * h, PUSH>(p, coff, nvec, lane);
     else if (n <= 5) read_fold_all<T, OPC, 4, 4 - h, PUSH>(p, coff, nvec, lane);
     else read_fold_all<T, OPC, 7, 3 - h, PUSH>(p, coff, nvec, lane);
@@ -755,11 +816,12 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
   __builtin_amdgcn_wave_barrier();
   // START to every peer, then wait for theirs
   if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + 1);
-  for (int k = 1; k < n; ++k) {
-    const int q = direct_peer(n, r, k);
-    if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx[q] + 1, ctl, lane)) goto aborted;
-  }
+  if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), rx[lane < n ? lane : 0] + 1, lane < n && lane != r, ctl))
+    goto aborted;
   acquire_sys(p.sys_fence);
+  if (PUSH && VEC && MNCCL_READ_STREAM && n <= 8 && read_push_stream<T, OPC>(p, w, A, lane)) {
+    // the whole chunk went as one stream (no per-iteration message in the push form)
+  } else
   for (uint32_t j = 0; j <= iters; ++j) {
     if (j < iters) {
       // F(j): fold my chunk's slice j from the peers' send buffers, store, drain, READY
@@ -767,14 +829,16 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
       const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
       const u64 coff = (u64)r * p.chunk_bytes + s * p.slice_bytes;
       const uint32_t pushed = len ? read_fold<T, OPC, VEC, PUSH>(p, coff, len, lane) : 0;
-      drain_stores();
       if (PUSH) {
+        // no READY (the peers wait only for DONE, which drains every push), so no drain per
+        // slice -- except before the part read back from my recv to be pushed
         if (pushed < len) {
-          read_push_rest<T, VEC>(p, coff, len, pushed, lane);
           drain_stores();
+          read_push_rest<T, VEC>(p, coff, len, pushed, lane);
         }
-        continue;  // no READY: the peers wait only for DONE
+        continue;
       }
+      drain_stores();
       if (p.sys_fence && lane == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + 2 + j);
     }
@@ -819,13 +883,115 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
     st_sys(p.peer_mbox[lane] + mbox_credit(n, C, r, w), rx[lane] + mpc);
     st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + mpc);
   }
-  for (int k = 1; k < n; ++k) {
-    const int q = direct_peer(n, r, k);
-    if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx[q] + mpc, ctl, lane)) goto aborted;
-  }
+  if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), rx[lane < n ? lane : 0] + mpc, lane < n && lane != r, ctl))
+    goto aborted;
   if (lane < n && lane != r) {
     p.tx_seq[(u64)lane * C + w] = tx[lane] + mpc;
     p.rx_seq[(u64)lane * C + w] = rx[lane] + mpc;
+  }
+  return;
+aborted:
+  if (lane == 0)
+    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), abort_word(p));
+}
+
+// ---------------------------------------------------------------- one-shot kernel
+// Small calls (schedule.h oneshot_fits): one hand-off instead of the ring's 2(n-1) dependent
+// ones.  Pipeline w = s * n + c owns slice s of chunk c: it stores that piece of its send into
+// every peer's scratch slot -- one message per (pair, pipeline) on the same FIFOs, READY words,
+// credits and counters as the ring (calls of either schedule follow each other freely) -- and,
+// once every peer's piece is in, folds the piece of the result itself in ring order: x_c, then
+// acc = op(x_q, acc) for q = c+1, ..., c-1 (the read schedule's order, the reference ring's
+// association), so every rank computes every element exactly as the ring does.  The n
+// pipelines of a slice run side by side: a 4 KiB call at 8 ranks is 8 waves, each one piece
+// out, one flag round, one fold.  Costs (n-1) x the call's bytes out per rank: small calls only.
+template <typename T, int OPC, bool VEC>
+__global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) oneshot_kernel(CollParams p) {
+  signal_start(p);
+  const WaveId id = wave_id();
+  const int lane = id.lane, w = id.w, C = p.pipes, wv = id.wv;
+  const int n = p.n, r = p.rank, K = p.nslots;
+  copy_tail(p, w, lane);
+  __shared__ u64 s_tx[kMaxWaves][kMaxRanks], s_rx[kMaxWaves][kMaxRanks];
+  u64* tx = s_tx[wv];
+  u64* rx = s_rx[wv];
+  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox};
+  if (lane < n) {
+    tx[lane] = p.tx_seq[(u64)lane * C + w];
+    rx[lane] = p.rx_seq[(u64)lane * C + w];
+  }
+  __builtin_amdgcn_wave_barrier();
+  const bool peer = lane < n && lane != r;  // lane q speaks for peer q
+  const u64 mytx = tx[lane < n ? lane : 0], myrx = rx[lane < n ? lane : 0];
+  const int c = w % n;
+  const u64 s = (u64)(w / n);
+  const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
+  const u64 coff = (u64)c * p.chunk_bytes + s * p.slice_bytes;
+  const uint32_t nvec = VEC ? len >> 4 : 0;
+  typedef typename Scal<sizeof(T)>::U U;
+  const uint32_t ne = len / (uint32_t)sizeof(T), e0 = nvec * 16 / (uint32_t)sizeof(T);
+  const rsrc_t mine = make_rsrc(p.send + coff, len);
+  // my message's slot in every peer must be free (the peer consumed message tx - slots)
+  if (!wave_wait_peers(p.mbox + mbox_credit(n, C, lane, w), mytx + 1 - (u64)K, peer && mytx + 1 > (u64)K, ctl))
+    goto aborted;
+  // my piece into every peer's slot
+  for (uint32_t i = (uint32_t)lane; i < nvec; i += 64) {
+    const v4u v = ld_slot16(mine, i * 16);
+    for (int k = 1; k < n; ++k) {
+      const int q = direct_peer(n, r, k);
+      st_slot16(make_rsrc(msg_slot(p, C, r, q, w, tx[q]), len), i * 16, v);
+    }
+  }
+  for (uint32_t e = e0 + (uint32_t)lane; e < ne; e += 64) {
+    const U v = Scal<sizeof(T)>::ld(mine, e * (uint32_t)sizeof(T));
+    for (int k = 1; k < n; ++k) {
+      const int q = direct_peer(n, r, k);
+      Scal<sizeof(T)>::st(make_rsrc(msg_slot(p, C, r, q, w, tx[q]), len), e * (uint32_t)sizeof(T), v);
+    }
+  }
+  drain_stores();
+  if (p.sys_fence && lane == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (peer) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), mytx + 1);
+  // every peer's piece, then the fold: in[k] = rank c + k's piece (my own send for me)
+  if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), myrx + 1, peer, ctl)) goto aborted;
+  acquire_sys(p.sys_fence);
+  if (len) {
+    rsrc_t in[kMaxRanks];
+#pragma unroll
+    for (int k = 0; k < kMaxRanks; ++k)
+      if (k < n) {
+        const int q = mod_n(c + k, n);
+        in[k] = q == r ? mine : make_rsrc(msg_slot(p, C, q, r, w, rx[q]), len);
+      }
+    const rsrc_t out = make_rsrc(p.recv + coff, len);
+    for (uint32_t i = (uint32_t)lane; i < nvec; i += 64) {
+      v4u x[kMaxRanks];
+#pragma unroll
+      for (int k = 0; k < kMaxRanks; ++k)
+        if (k < n) x[k] = ld_slot16(in[k], i * 16);
+      v4u acc = x[0];
+#pragma unroll
+      for (int k = 1; k < kMaxRanks; ++k)
+        if (k < n) acc = reduce16<T, OPC>(x[k], acc);
+      st_nt16(out, i * 16, acc);
+    }
+    for (uint32_t e = e0 + (uint32_t)lane; e < ne; e += 64) {
+      U x[kMaxRanks];
+#pragma unroll
+      for (int k = 0; k < kMaxRanks; ++k)
+        if (k < n) x[k] = Scal<sizeof(T)>::ld(in[k], e * (uint32_t)sizeof(T));
+      U acc = x[0];
+#pragma unroll
+      for (int k = 1; k < kMaxRanks; ++k)
+        if (k < n) acc = __builtin_bit_cast(U, Op<T, OPC>::f(__builtin_bit_cast(T, x[k]), __builtin_bit_cast(T, acc)));
+      Scal<sizeof(T)>::st(out, e * (uint32_t)sizeof(T), acc);
+    }
+  }
+  drain_stores();  // every load of the peers' pieces has returned: their slots are free again
+  if (peer) {
+    st_sys(p.peer_mbox[lane] + mbox_credit(n, C, r, w), myrx + 1);
+    p.tx_seq[(u64)lane * C + w] = mytx + 1;
+    p.rx_seq[(u64)lane * C + w] = myrx + 1;
   }
   return;
 aborted:
@@ -1028,6 +1194,27 @@ hipError_t launch_ring(int dtype, int op, bool vec, int C, int nt, const CollPar
 
 hipError_t launch_read(int dtype, int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
 #define M(T) return read_for_t<T>(op, vec, C, nt, p, st)
+  MNCCL_DISPATCH_T(dtype, M)
+#undef M
+}
+
+template <typename T>
+static hipError_t oneshot_for_t(int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
+#define ONESHOT_CASE(OPC)                                                                           \
+  case OPC:                                                                                         \
+    if (vec) hipLaunchKernelGGL((oneshot_kernel<T, OPC, true>), dim3(C), dim3(nt), 0, st, p);      \
+    else hipLaunchKernelGGL((oneshot_kernel<T, OPC, false>), dim3(C), dim3(nt), 0, st, p);         \
+    break;
+  switch (op) {
+    ONESHOT_CASE(kSum) ONESHOT_CASE(kProd) ONESHOT_CASE(kMax) ONESHOT_CASE(kMin)
+    default: return hipErrorInvalidValue;
+  }
+#undef ONESHOT_CASE
+  return hipGetLastError();
+}
+
+hipError_t launch_oneshot(int dtype, int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
+#define M(T) return oneshot_for_t<T>(op, vec, C, nt, p, st)
   MNCCL_DISPATCH_T(dtype, M)
 #undef M
 }

@@ -148,6 +148,23 @@ MNCCL_HD uint64_t read_slice(uint64_t chunk_bytes, int C, uint64_t slice, uint64
   return s;
 }
 
+// One-shot (kernels.hip oneshot_kernel): pipeline w = s * n + c carries slice s of chunk c --
+// its message to every peer is that piece of this rank's send, and it folds that piece of the
+// result from all n ranks' pieces.  A call takes it when its n x nslices pipelines fit one round
+// (n x nslices <= C) and its bytes (n chunks) are at most kOneShotMaxBytes -- or at any size that
+// fits when forced (MINI_NCCL_ALGO=oneshot).  Each rank sends (n - 1) x the call's bytes: a
+// latency path, not a bandwidth one.
+constexpr uint64_t kOneShotMaxBytes = 64u << 10;
+MNCCL_HD uint64_t oneshot_slice(uint64_t chunk_bytes, int n, int C, uint64_t slot_bytes) {
+  const int per = n > 0 && C / n > 0 ? C / n : 1;
+  return effective_slice(chunk_bytes, per, slot_bytes, kMinSlice, 1);
+}
+MNCCL_HD bool oneshot_fits(uint64_t chunk_bytes, int n, int C, uint64_t slot_bytes, bool forced) {
+  if (n < 2 || chunk_bytes == 0 || (!forced && chunk_bytes * (uint64_t)n > kOneShotMaxBytes)) return false;
+  const uint64_t sl = oneshot_slice(chunk_bytes, n, C, slot_bytes);
+  return sl <= slot_bytes && (chunk_bytes + sl - 1) / sl * (uint64_t)n <= (uint64_t)C;
+}
+
 // Scratch layout: one region per PEER rank (n - 1 of them: the owner never sends to itself),
 // [C][slots][slice_bytes] each.  region_index maps a peer rank q != owner to its region.
 MNCCL_HD uint64_t scratch_region_bytes(int C, int slots, uint64_t slice_bytes) { return (uint64_t)C * slots * slice_bytes; }

@@ -1,4 +1,4 @@
-// sim.cpp -- host-side simulator of the ring / read kernels' protocol, for the CPU test
+// sim.cpp -- host-side simulator of the ring / read / one-shot kernels' protocol, for the CPU test
 // suite (no GPU).  Each (rank, channel) runs the same op sequence as kernels.hip, using the
 // same schedule.h index math, scratch layout and mailbox layout; a wait that is not
 // satisfied yields, and the scheduler round-robins over all programs.  It checks:
@@ -193,9 +193,66 @@ bool read_step(World& W, Prog& P) {
   }
 }
 
+// One step of the one-shot schedule (kernels.hip oneshot_kernel): pipeline w = s * n + c owns
+// slice s of chunk c.  Stage 0 waits for every peer's credit, stores that piece of its send into
+// every peer's slot and raises READY; stage 1 waits for every peer's READY, folds the piece in
+// ring order from the slots (its own piece from its send) into recv and returns the credits.
+bool oneshot_step(World& W, Prog& P) {
+  const int n = W.n, r = P.r, w = P.w, K = W.K;
+  auto tx = [&](int d) { return W.tx_seq[r][(size_t)d * W.C + w]; };
+  auto rx = [&](int q) { return W.rx_seq[r][(size_t)q * W.C + w]; };
+  const int c = w % n;
+  const uint64_t s = (uint64_t)(w / n);
+  const uint64_t len = slice_len(W.chunk_bytes, W.slice, s), coff = (uint64_t)c * W.chunk_bytes + s * W.slice;
+  if (P.j == 0) {
+    for (int k = 1; k < n; ++k) {
+      const int q = direct_peer(n, r, k);
+      if (tx(q) + 1 > (uint64_t)K && W.credit(r, q, w) < tx(q) + 1 - K) return false;
+    }
+    for (int k = 1; k < n; ++k) {
+      const int q = direct_peer(n, r, k);
+      if (len) memcpy(W.slot(r, q, w, tx(q)), (const char*)W.send[r] + coff, len);
+      W.ready(q, r, w) = tx(q) + 1;
+    }
+    P.j = 1;
+    return true;
+  }
+  for (int k = 1; k < n; ++k) {
+    const int q = direct_peer(n, r, k);
+    if (W.ready(r, q, w) < rx(q) + 1) return false;
+  }
+  auto piece = [&](int q) -> const float* {
+    return (const float*)(q == r ? (const char*)W.send[r] + coff : W.slot(q, r, w, rx(q)));
+  };
+  if (len) {
+    // every piece is read before recv's (in place: send's) piece is written
+    std::vector<float> res((size_t)(len / 4));
+    for (uint64_t i = 0; i < len / 4; ++i) {
+      float acc = piece(c)[i];
+      for (int k = 1; k < n; ++k) acc = apply(W.op, piece(direct_peer(n, c, k))[i], acc);
+      res[(size_t)i] = acc;
+    }
+    memcpy((char*)W.recv[r] + coff, res.data(), (size_t)len);
+  }
+  for (int k = 1; k < n; ++k) {
+    const int q = direct_peer(n, r, k);
+    W.credit(q, r, w) = rx(q) + 1;
+  }
+  P.done = true;
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
+
+// csrc/schedule.h one-shot geometry, exported for the host-logic tests
+uint64_t mnccl_oneshot_slice(uint64_t chunk_bytes, int n, int channels, uint64_t slot_bytes) {
+  return oneshot_slice(chunk_bytes, n, channels, slot_bytes);
+}
+int mnccl_oneshot_fits(uint64_t chunk_bytes, int n, int channels, uint64_t slot_bytes, int forced) {
+  return oneshot_fits(chunk_bytes, n, channels, slot_bytes, forced != 0) ? 1 : 0;
+}
 
 // csrc/schedule.h effective_slice, exported for the host-logic tests
 uint64_t mnccl_effective_slice(uint64_t chunk_bytes, int channels, uint64_t slice, uint64_t min_slice, int depth) {
@@ -220,8 +277,9 @@ int mnccl_call_pipelines(uint64_t nslices, int channels, int waves) { return cal
 
 // Runs `calls` consecutive all-reduces (send -> recv, fp32; send == recv for in place) on n
 // simulated ranks with the GPU kernels' protocol; call i uses schedule (algo >> 2i) & 3 (0 ring,
-// 2 read in its push form, 3 read in its load form; schedules can alternate on one communicator
-// state, as mncclCommSetAlgo allows).  schedule_seed != 0 permutes the order programs are tried
+// 1 one-shot, 2 read in its push form, 3 read in its load form; schedules can alternate on one
+// communicator state, as mncclCommSetAlgo allows).  A one-shot call's slice: oneshot_slice when
+// min_slice != 0 (Comm::launch; -2 if the call does not fit), else the slot.  schedule_seed != 0 permutes the order programs are tried
 // in (pseudo-random), exploring different interleavings.  min_slice: 0 = fixed payload (the
 // configured slice), else the adaptive payload of Comm::launch.  Returns 0, -1 on deadlock,
 // -2 on bad arguments.  *steps_out = ops executed.
@@ -229,8 +287,6 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
                         uint64_t slice_bytes, uint64_t min_slice, int channels, int slots, int calls,
                         uint64_t schedule_seed, uint64_t* steps_out) {
   if (n < 1 || n > 16 || channels < 1 || slots < 1 || slice_bytes < 4 || slice_bytes % 4) return -2;
-  for (int call = 0; call < calls; ++call)
-    if (((algo >> (2 * call)) & 3) == 1) return -2;  // the direct schedule is gone (4.0)
   World W;
   W.n = n; W.C = channels; W.K = slots; W.op = op; W.algo = (int)algo; W.slot_bytes = slice_bytes;
   const uint64_t chunk = count / (uint64_t)n;
@@ -246,15 +302,19 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
   uint64_t rng = schedule_seed * 6364136223846793005ull + 1442695040888963407ull;
   for (int call = 0; call < calls; ++call) {
     const int code = (int)((algo >> (2 * call)) & 3);
-    const int a = code >= 2 ? 2 : 0;
+    const int a = code >= 2 ? 2 : code;  // 0 ring, 1 one-shot, 2 read
     W.push = code == 2;
     // as Comm::launch: adaptive payload (min_slice 0 = off; the read schedule's own rule), fixed
     // slot stride, one pipeline per slice up to all of them
-    if (!min_slice) W.slice = slice_bytes;
+    if (a == 1 && W.chunk_bytes) {
+      if (min_slice && !oneshot_fits(W.chunk_bytes, n, channels, slice_bytes, true)) return -2;
+      W.slice = min_slice ? oneshot_slice(W.chunk_bytes, n, channels, slice_bytes) : slice_bytes;
+      if ((W.chunk_bytes + W.slice - 1) / W.slice * (uint64_t)n > (uint64_t)channels) return -2;
+    } else if (!min_slice || a == 1) W.slice = slice_bytes;
     else if (a == 2) W.slice = read_slice(W.chunk_bytes, channels, slice_bytes, min_slice, kReadDepth);
     else W.slice = effective_slice(W.chunk_bytes, channels, slice_bytes, min_slice, 1);
     W.nslices = (W.chunk_bytes + W.slice - 1) / W.slice;
-    W.A = call_pipelines(W.nslices, channels, 1);
+    W.A = call_pipelines(a == 1 ? W.nslices * (uint64_t)n : W.nslices, channels, 1);  // one-shot: per chunk too
     W.iters = (uint32_t)((W.nslices + (uint64_t)W.A - 1) / (uint64_t)W.A);
     for (int r = 0; r < n; ++r) {  // send -> recv copy of the tail (Comm::allreduce)
       if ((const void*)recv[r] == (const void*)send[r]) continue;  // in place
@@ -286,7 +346,7 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
           burst = 1 + (int)((rng >> 40) % 4);
         }
         for (int b = 0; b < burst && !P.done; ++b) {
-          const bool ok = a == 2 ? read_step(W, P) : ring_step(W, P);
+          const bool ok = a == 2 ? read_step(W, P) : a == 1 ? oneshot_step(W, P) : ring_step(W, P);
           if (!ok) break;
           any = true;
           ++steps;
@@ -299,11 +359,12 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
     // the kernels' last action per pipeline that ran: advance the per-pair FIFO counters
     for (int r = 0; r < n; ++r)
       for (int w = 0; w < W.A; ++w) {
-        if (a == 2) {
+        if (a == 2 || a == 1) {
+          const uint64_t m = a == 2 ? read_msgs_per_call(W.iters) : 1;  // one-shot: one message each way
           for (int q = 0; q < n; ++q) {
             if (q == r) continue;
-            W.tx_seq[r][(size_t)q * channels + w] += read_msgs_per_call(W.iters);
-            W.rx_seq[r][(size_t)q * channels + w] += read_msgs_per_call(W.iters);
+            W.tx_seq[r][(size_t)q * channels + w] += m;
+            W.rx_seq[r][(size_t)q * channels + w] += m;
           }
         } else {
           const uint64_t m = (uint64_t)W.iters * ring_msgs_per_iter(n);

@@ -36,7 +36,7 @@ ncclFloat16, ncclFloat, ncclDouble, ncclBfloat16 = 6, 7, 8, 9
 ncclSum, ncclProd, ncclMax, ncclMin, ncclAvg = 0, 1, 2, 3, 4
 
 # mncclAlgo_t (mncclAlgoDirect = 1 was removed in mncclVersion 400)
-ALGO_AUTO, ALGO_RING, ALGO_READ = -1, 0, 2
+ALGO_AUTO, ALGO_RING, ALGO_READ, ALGO_ONESHOT = -1, 0, 2, 3
 
 DTYPE_SIZE = {ncclInt32: 4, ncclFloat16: 2, ncclFloat: 4, ncclDouble: 8, ncclBfloat16: 2}
 

@@ -63,6 +63,16 @@ int main() {
             ++fails;
           }
         }
+  // the one-shot schedule: a slot holds n pieces, so a larger slot and 64 pipelines
+  for (int n = 2; n <= 8; n += 3)
+    for (uint64_t c : counts)
+      for (int adaptive = 0; adaptive < 2; ++adaptive) {
+        const int rc = sim_case(1, n, c, 16384, adaptive ? 64 : 0, 64, 2 + (int)(c % 2), 3, c + (uint64_t)n);
+        if (rc) {
+          printf("sim FAIL one-shot n=%d count=%llu adaptive=%d rc=%d\n", n, (unsigned long long)c, adaptive, rc);
+          ++fails;
+        }
+      }
   // bootstrap: 3 ranks as threads over loopback
   const char* pe = getenv("SELFTEST_PORT");
   const int port = pe ? atoi(pe) : 29471;

@@ -24,6 +24,9 @@ def load():
         L.mnccl_read_slice.argtypes = [u64, i, u64, u64, i]
         L.mnccl_read_slice.restype = u64
         L.mnccl_call_pipelines.argtypes = [u64, i, i]
+        L.mnccl_oneshot_slice.argtypes = [u64, i, i, u64]
+        L.mnccl_oneshot_slice.restype = u64
+        L.mnccl_oneshot_fits.argtypes = [u64, i, i, u64, i]
         L.mnccl_effective_slice.argtypes = [u64, i, u64, u64, i]
         L.mnccl_effective_slice.restype = u64
         L.mnccl_bootstrap_selftest.argtypes = [i, i, ctypes.c_char_p, i, i]
@@ -33,7 +36,8 @@ def load():
     return _lib
 
 
-RING, READ, READ_LOAD = 0, 2, 3  # schedules: the ring, read in its push form, read in its load form
+# schedules: the ring, the one-shot, read in its push form, read in its load form
+RING, ONESHOT, READ, READ_LOAD = 0, 1, 2, 3
 
 
 def allreduce(inputs, algo=0, op=0, slice_bytes=1024, channels=4, slots=2, calls=1, seed=0, algos=None, min_slice=0,
@@ -83,6 +87,14 @@ def effective_slice(chunk_bytes, channels, slice_bytes, min_slice, depth=1):
 
 def read_slice(chunk_bytes, channels, slice_bytes, min_slice, depth=16):
     return load().mnccl_read_slice(chunk_bytes, channels, slice_bytes, min_slice, depth)
+
+
+def oneshot_slice(chunk_bytes, n, channels, slot_bytes):
+    return load().mnccl_oneshot_slice(chunk_bytes, n, channels, slot_bytes)
+
+
+def oneshot_fits(chunk_bytes, n, channels, slot_bytes, forced=False):
+    return bool(load().mnccl_oneshot_fits(chunk_bytes, n, channels, slot_bytes, int(forced)))
 
 
 def call_pipelines(nslices, channels, waves=1):

@@ -80,6 +80,11 @@ def _run_allreduce(n, cases, env=None, timeout=300, barrier=True):
             dev_bufs = all(c.get(k, "device") == "device" for k in ("mem", "recv_mem"))
             if c["algo"] == 2 and dev_bufs and c["count"] >= n:
                 assert res["last_algo"] == 2, f"rank {r} case {c}: ran schedule {res['last_algo']}"
+            # forced one-shot: every case of the tests below fits it
+            if c["algo"] == 3 and c["count"] >= n:
+                assert res["last_algo"] == 3, f"rank {r} case {c}: ran schedule {res['last_algo']}"
+            if "expect_algo" in c:
+                assert res["last_algo"] == c["expect_algo"], f"rank {r} case {c}: ran schedule {res['last_algo']}"
             # no IPC open ever failed (nothing retries: a failure would send a call to the
             # ring, csrc/peerbuf.cpp), in this process or in any rank's mapping round
             assert res["ipc_open_failures"] == 0 and res["read_map_failures"] == 0, (r, c, res)
@@ -146,8 +151,9 @@ def test_auto_schedule_no_init_allreduce(dev):
     assert all("error" not in out[r] for r in range(3)), out
     for r in range(3):
         i = out[r]["info"]
-        # auto = the read schedule; its fallback for buffers that cannot be shared: the ring here
-        assert i["tune_ms"] == [0.0, 0.0] and i["algo"] == 2 and i["scratch_algo"] == 0, i
+        # auto (-1): one-shot for small calls, then the read schedule; its fallback for buffers
+        # that cannot be shared: the ring here
+        assert i["tune_ms"] == [0.0, 0.0] and i["algo"] == -1 and i["scratch_algo"] == 0, i
         assert i["read_push"] == 1 and i["calib_choice"] == -1 and i["calib_ms"] == [0.0, 0.0], i
         assert i["ranks_on_device"] == 3 and i["last_algo"] == -1, i
         assert i["channels"] == 256 and i["pipelines"] == 256 and i["slot_bytes"] == 128 << 10
@@ -234,6 +240,45 @@ def test_allreduce_dtypes_ops(dev, sched):
     cases = [_case(dtype=d, op=o, count=50000 + 7 * i, algo=algo, seed=100 + i, special=o in ("max", "min"))
              for i, (d, o) in enumerate((d, o) for d in DTYPES for o in OPS)]
     _run_allreduce(3, cases, env)
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_oneshot_parity(dev, n):
+    # the one-shot schedule (small calls; forced here so larger calls that fit a slot per pipeline
+    # take it too): every dtype x op, tails of count % n, in place, the scalar path (odd 2-byte
+    # chunks, a misaligned base), repeated calls on varying data -- bit-exact vs the oracle, the
+    # reference ring's association order
+    cases = [_case(dtype=d, op=o, count=n * 997 + i % n, algo=3, seed=700 + i, special=o in ("max", "min"),
+                   inplace=(i % 3 == 1)) for i, (d, o) in enumerate((d, o) for d in DTYPES for o in OPS)]
+    cases += [_case(count=n * 1024, algo=3, seed=720),                          # one 1 KiB piece
+              _case(count=(1 << 18) + 3, algo=3, seed=721, inplace=True),       # many pipelines, tail
+              _case(dtype="f16", count=n * 333 + 1, algo=3, seed=722),          # odd chunks: scalar path
+              _case(count=12345, algo=3, seed=723, offset=2),                   # misaligned: scalar path
+              _case(count=n - 1, algo=3, seed=724),                             # count < n: copy only
+              _case(count=5000, algo=3, calls=5, seed=725, vary=True)]          # slots and credits reused
+    _run_allreduce(n, cases, timeout=600)
+
+
+def test_schedules_interleaved_on_one_communicator(dev):
+    # the one-shot, the ring and the read schedule share the per-(pair, pipeline) FIFO counters,
+    # READY words, credits and scratch slots: calls of all three (and auto's choice by size)
+    # alternate on one communicator, on changing data, every call checked
+    n = 4
+    plan = [(3, 3000), (0, 70001), (2, 1 << 18), (-1, 4096), (3, 16384), (0, 1000), (-1, 1 << 20), (2, 777),
+            (3, 100003), (-1, 65536 // 4), (0, 5), (3, 8 * 1024)]
+    cases = [_case(count=c, algo=a, calls=2, vary=True, seed=800 + i, inplace=(i % 2 == 0),
+                   **({"expect_algo": 3} if a == -1 and c * 4 <= 64 << 10 else {})) for i, (a, c) in enumerate(plan)]
+    _run_allreduce(n, cases, timeout=600)
+
+
+@pytest.mark.parametrize("mem", ["pinned", "pageable"])
+def test_oneshot_host_buffers(dev, mem):
+    # auto's small calls on host buffers (the ring's domain before one-shot): pinned memory read
+    # and written through its device mapping, pageable memory staged through HBM
+    cases = [_case(count=4099, algo=-1, mem=mem, seed=30, expect_algo=3),
+             _case(count=3 * 5000 + 2, algo=-1, mem=mem, inplace=True, seed=31, expect_algo=3),
+             _case(dtype="bf16", count=3001, algo=-1, mem=mem, recv_mem="device", seed=32, expect_algo=3)]
+    _run_allreduce(3, cases)
 
 
 def test_read_schedule_count_mismatch_is_invalid_usage(dev):

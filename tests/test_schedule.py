@@ -99,6 +99,53 @@ def test_sim_switching_schedules_on_one_communicator(oracle_lib, sim_lib, algos,
     assert all(same_bits(g, e) for g, e in zip(got, ref))
 
 
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+@pytest.mark.parametrize("count", [7, 1000, 4099, 70001])
+@pytest.mark.parametrize("inplace", [False, True], ids=["out", "inplace"])
+def test_sim_oneshot(oracle_lib, sim_lib, n, count, inplace):
+    # the one-shot schedule (kernels.hip oneshot_kernel): every rank folds all n chunks from the
+    # peers' messages in ring order -- the reference ring's bits on every rank, 3 calls on one
+    # communicator state (slots and credits reused), random interleavings
+    xs = O.random_inputs(n, count, "f32", seed=count + n)
+    ref = O.allreduce(xs, slice_bytes=1024)
+    if inplace:  # every call after the first reduces the previous result
+        ref = O.allreduce(ref, slice_bytes=1024)
+        ref = O.allreduce(ref, slice_bytes=1024)
+    got, _ = S.allreduce(xs, algo=S.ONESHOT, slice_bytes=16384, min_slice=1024, channels=64, slots=2, calls=3,
+                         seed=count, inplace=inplace)
+    assert all(same_bits(g, e) for g, e in zip(got, ref))
+
+
+@pytest.mark.parametrize("algos", [[1, 0, 1, 2], [3, 1, 1, 0, 2], [0, 0, 1], [2, 1, 2, 3, 1], [1, 2, 2, 0, 1, 1]])
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+def test_sim_oneshot_switching_schedules(oracle_lib, sim_lib, algos, n):
+    # the one-shot shares the per-(pair, pipeline) FIFO counters, READY words, credits and slots
+    # with the ring and the read schedule: any order of calls keeps every link consistent
+    xs = O.random_inputs(n, 9001, "f32", seed=3 * n)
+    ref = O.allreduce(xs, slice_bytes=1024)
+    for seed in (0, 5, 11):
+        got, _ = S.allreduce(xs, slice_bytes=16384, min_slice=1024, channels=64, slots=2, algos=algos, seed=seed)
+        assert all(same_bits(g, e) for g, e in zip(got, ref)), seed
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8, 16])
+@pytest.mark.parametrize("chunk", [4, 1000, 4096, 8192, 1 << 15, 100000, 1 << 20, 1 << 24])
+def test_oneshot_geometry(sim_lib, n, chunk):
+    # schedule.h oneshot_slice / oneshot_fits: a pipeline per slice of every chunk, one round of
+    # the pipelines covers the call, a piece fits a slot, whole 1 KiB waves; auto takes it only up
+    # to 64 KiB per call
+    C, slot = 256, 128 << 10
+    sl = S.oneshot_slice(chunk, n, C, slot)
+    forced, auto = S.oneshot_fits(chunk, n, C, slot, True), S.oneshot_fits(chunk, n, C, slot, False)
+    assert sl % 1024 == 0 and 1024 <= sl <= slot
+    if forced:
+        assert -(-chunk // sl) * n <= C
+    assert auto == (forced and chunk * n <= 64 << 10)
+    if chunk * n <= 64 << 10 and n <= 16:
+        assert auto  # every call the auto path meant for one-shot fits the default geometry
+    assert not S.oneshot_fits(chunk, 1, C, slot, True)
+
+
 @pytest.mark.parametrize("chunk", [0, 4, 1000, 1 << 16, (1 << 20) + 12, 3 << 22, 1 << 27, 1 << 30])
 @pytest.mark.parametrize("C", [1, 7, 256])
 def test_effective_slice_properties(sim_lib, chunk, C):

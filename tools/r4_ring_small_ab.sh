@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 AB_DIR=${AB_DIR:-$R/build_ab}
 SIZES=${SIZES:-4k,64k,1}
 ITERS=${ITERS:-200}
-export GPU_MAX_HW_QUEUES=2 MINI_NCCL_PERF_DEVICE=0
+export GPU_MAX_HW_QUEUES=${QUEUES:-2} MINI_NCCL_PERF_DEVICE=0
 run() {
   local nr="$1" tag="$2"; shift 2
   local port=$((20000 + RANDOM % 20000))

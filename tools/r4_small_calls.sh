@@ -2,9 +2,9 @@
 # Small-call time at 2 / 4 / 8 rank processes sharing one GPU, ring and read (push form) and the
 # read schedule's load form (perf_test rank 0, 200 blocking calls per size): the round-4 library.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-export GPU_MAX_HW_QUEUES=2 MINI_NCCL_PERF_DEVICE=0
+export GPU_MAX_HW_QUEUES=${QUEUES:-2} MINI_NCCL_PERF_DEVICE=0
 for nr in ${NRS:-2 4 8}; do
-  for cfg in ring:1 read:1 read:0; do
+  for cfg in ${CFGS:-ring:1 read:1 read:0 oneshot:1}; do
     algo=${cfg%%:*}; push=${cfg#*:}
     port=$((21000 + RANDOM % 20000))
     pids=()
