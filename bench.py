@@ -357,6 +357,7 @@ def size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks, 
         ok = comm.async_error() == 0
         ours()
         torch.cuda.synchronize()
+        row["schedule"] = {0: "ring", 2: "read", 3: "oneshot"}.get(comm.info()["last_algo"], "?")
         row["ok"] = max_over_ranks(0.0 if (ok and bool((r_ == float(n)).all().item())) else 1.0) == 0.0
         rows.append(row)
     return rows

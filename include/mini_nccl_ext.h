@@ -31,13 +31,13 @@ extern "C" {
    MINI_NCCL_TUNE removed; 400 the direct schedule and MINI_NCCL_PULL / DIRECT_OVERLAP /
    CALIBRATE / PIPE_DEPTH / MIN_SLICE / STAGE_HOST removed, MINI_NCCL_READ_PUSH added, the ring
    runs only the pipelines a call's slices need, mncclCommInfo_t grew again (same prefix);
-   401 the one-shot schedule (mncclAlgoOneShot, auto for small calls) */
+   401 the one-shot schedule (mncclAlgoOneShot; auto's small calls that would run the ring) */
 #define MNCCL_VERSION 401
 
 /* schedules; all produce bit-identical results (same fold order per element) */
 typedef enum {
-  mncclAlgoAuto = -1,  /* the library's default: one-shot for calls of at most 64 KiB, read for
-                          device buffers every rank can share, the ring for every other call */
+  mncclAlgoAuto = -1,  /* the library's default: read for device buffers every rank can share;
+                          every other call one-shot when at most 64 KiB, else the ring */
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
   mncclAlgoDirect = 1, /* removed in 400 (never faster than the ring); mncclCommSetAlgo and
                           MINI_NCCL_ALGO reject it */
@@ -54,9 +54,10 @@ typedef enum {
   mncclAlgoOneShot = 3 /* since 401, small calls: every rank stores its whole input into every
                           peer's scratch in one message per pipeline and folds all n chunks
                           itself in the same order -- one hand-off instead of the ring's
-                          2(n-1).  mncclAlgoAuto takes it for calls of at most 64 KiB; forced,
-                          every call whose slices fit one scratch slot per pipeline (the others
-                          run as with mncclAlgoAuto) */
+                          2(n-1).  mncclAlgoAuto takes it for calls of at most 64 KiB that the
+                          read schedule cannot take (host buffers, a full export table); forced,
+                          every call whose pieces fit one round of the pipelines (the others run
+                          as with mncclAlgoAuto) */
 } mncclAlgo_t;
 
 typedef struct {

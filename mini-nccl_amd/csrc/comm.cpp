@@ -542,10 +542,14 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     // buffers the read schedule already shares (live exports of this process, checked by reap())
     // need no pointer query: device memory of this GPU
     bool local_s = false, local_r = false;
-    // one-shot for small calls (auto) or wherever a call fits it (forced); then the read schedule
-    // where every rank can share its buffers, the ring otherwise -- a pure function of the call's
-    // size and the rank-uniform config up to the read rendezvous, which all ranks decide alike
-    const bool oneshot = (auto_ || algo_ == 3) && oneshot_fits(chunk_bytes, n, wave_channels(), wave_slice(), !auto_);
+    // forced one-shot wherever a call fits it; otherwise the read schedule where every rank can
+    // share its buffers, and for the other calls the ring -- or, under auto, the one-shot for
+    // small ones (its one hand-off against the ring's 2(n-1); on the proxy the read schedule
+    // still wins at 8 ranks, profiles/r4_small_calls.txt, so auto keeps read first).  A pure
+    // function of the call's size and the rank-uniform config up to the read rendezvous, which
+    // all ranks decide alike.
+    const bool oneshot = algo_ == 3 && oneshot_fits(chunk_bytes, n, wave_channels(), wave_slice(), true);
+    const bool small = auto_ && oneshot_fits(chunk_bytes, n, wave_channels(), wave_slice(), false);
     const bool read_sched = !oneshot && (algo_ == 2 || algo_ == 3) && pbuf_.available();
     if (read_sched) pbuf_.reap(send, recv);
     const Reach rs = read_sched && pbuf_.known(send) ? (local_s = true, Reach::kDevice) : reach(send, &ksend, &local_s);
@@ -612,6 +616,7 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
         vec = vec_all && (chunk_bytes % 4 == 0);
       }
     }
+    if (algo == 0 && small) algo = 3;
     seq = ++call_seq_;
     if (seq == 0) seq = ++call_seq_;  // 0 = "no kernel" (wait_for)
     launch(algo, ksend, krecv, chunk_bytes, dtype, op, stream, seq, vec, psend, precv, tail);

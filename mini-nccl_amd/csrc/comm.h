@@ -33,8 +33,8 @@ class Comm {
   int device() const { return device_; }
   const Config& config() const { return cfg_; }
   int algo() const { return auto_ ? -1 : algo_; }
-  // a < 0: the default (one-shot for small calls, read for buffers every rank can share, the
-  // ring for the other calls); 0 ring, 2 read, 3 one-shot wherever a call fits it
+  // a < 0: the default (read for buffers every rank can share; for the other calls the one-shot
+  // when small, else the ring); 0 ring, 2 read, 3 one-shot wherever a call fits it
   void set_algo(int a) {
     auto_ = a < 0;
     algo_ = a < 0 ? 2 : a;
@@ -80,7 +80,7 @@ class Comm {
   Geometry geo_;
   int algo_ = 0;                 // 0 ring, 2 read (its calls fall back to the ring when some rank's
                                  // buffers cannot be shared), 3 one-shot (larger calls: as auto)
-  bool auto_ = true;             // the default: small calls one-shot, the others as algo_ = 2
+  bool auto_ = true;             // the default: as algo_ = 2, with the ring's small calls one-shot
   int last_algo_ = -1;
   int ranks_on_device_ = 1;
   uint32_t call_seq_ = 0;        // kernel launches of this communicator (the kernel's start word)

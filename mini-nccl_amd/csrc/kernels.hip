@@ -589,9 +589,6 @@ __device__ __forceinline__ void read_copy_wide(const CollParams& p, uint64_t sof
 #ifndef MNCCL_READ_FOLD_ALL
 #define MNCCL_READ_FOLD_ALL 1
 #endif
-#ifndef MNCCL_READ_V2
-#define MNCCL_READ_V2 12  // vectors per lane per batch at 2 ranks (fp16 / bf16: 2/3 of it)
-#endif
 #ifndef MNCCL_FOLD_ALL_MIN_N
 #define MNCCL_FOLD_ALL_MIN_N 2
 #endif
@@ -608,16 +605,9 @@ __device__ __forceinline__ void read_copy_wide(const CollParams& p, uint64_t sof
 // (profiles/r3_read_push_ab.txt).  PUSH = false is the load form (READY per iteration, then every
 // peer's result slice loaded over the links), kept as the comparison form.
 
-template <typename T, bool VEC>
-__device__ __forceinline__ void read_push_rest(const CollParams& p, uint64_t coff, uint32_t nbytes, uint32_t off0,
-                                               int lane);
-
-// Batches b0, b0 + step, b0 + 2 step, ... (vector indices) below nvec: the slice form walks one
-// slice (b0 = 0, step = one batch); the stream form (MNCCL_READ_STREAM) walks the whole chunk with
-// the pipelines interleaved batch by batch (b0 = w batches, step = A batches).
 template <typename T, int OPC, int G, int V, bool PUSH>
-__device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff, uint32_t nvec, int lane,
-                                              uint32_t b0 = 0, uint32_t step = 64 * V) {
+__device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff, uint32_t nvec, int lane) {
+  constexpr uint32_t step = 64 * V;
   const int n = p.n, r = p.rank, w = wave_id().w;
   const uint32_t vb = nvec * 16;
   const rsrc_t loc = make_rsrc(p.send + coff, vb), out = make_rsrc(p.recv + coff, vb);
@@ -666,10 +656,8 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
   // wait vmcnt(0) where the two paths join -- for the prefetch itself and, as loads and stores
   // share vmcnt, for every store of the batch before: the double buffer then never overlapped
   // (tools/mix_probe.hip "persist2"; profiles/r4_vmcnt.txt).  A slice is at most kMaxSlice, so
-  // the past-the-end offsets stay below 2^32; in the stream form (a chunk below 4 GiB) one that
-  // wraps lands inside the same buffer: a wasted load whose registers are never read.
-  uint32_t b = b0;
-  if (b >= nvec) return;
+  // the past-the-end offsets stay below 2^32.
+  uint32_t b = 0;
   load(xa, aa, b);
   for (;;) {
     load(xb, ab, b + step);
@@ -679,39 +667,6 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
     fold_store(xb, ab, b);
     if ((b += step) >= nvec) break;
   }
-}
-
-// The push form's whole chunk r in one stream (MNCCL_READ_STREAM): the push form has no
-// per-iteration message, so its slices are only a way to deal work; here pipeline w takes
-// batches w, w + A, w + 2A, ... of the chunk (the A pipelines sweep one window of memory
-// together) with the next batch's loads in flight across what used to be slice boundaries.
-// False: the chunk is too large for one buffer resource (the caller runs the slice form).
-#ifndef MNCCL_READ_STREAM
-#define MNCCL_READ_STREAM 0
-#endif
-template <typename T, int OPC>
-__device__ __forceinline__ bool read_push_stream(const CollParams& p, int w, int A, int lane) {
-  if (p.chunk_bytes >= (1ull << 32) - 64) return false;
-  const int n = p.n;
-  const uint64_t coff = (uint64_t)p.rank * p.chunk_bytes;
-  const uint32_t nvec = (uint32_t)(p.chunk_bytes >> 4);
-  constexpr int h = sizeof(T) == 2 ? 1 : 0;
-#define STREAM(G, V) read_fold_all<T, OPC, G, V, true>(p, coff, nvec, lane, (uint32_t)w * 64u * (V), (uint32_t)A * 64u * (V))
-  if (nvec) {
-    if (n == 2) STREAM(1, MNCCL_READ_V2 - (MNCCL_READ_V2 / 3) * h);
-    else if (n == 3) STREAM(2, 8 - 2 * h);
-    else if (n <= 5) STREAM(4, 4 - h);
-    else STREAM(7, 3 - h);
-  }
-#undef STREAM
-  // the chunk's last chunk_bytes % 16 bytes: pipeline 0, element by element, then pushed
-  const uint32_t tail0 = nvec * 16u, cb = (uint32_t)p.chunk_bytes;
-  if (w == 0 && cb > tail0) {
-    read_fold_scalar<T, OPC>(p, coff, cb, lane, tail0);
-    drain_stores();
-    read_push_rest<T, true>(p, coff, cb, tail0, lane);
-  }
-  return true;
 }
 
 // Returns the leading bytes of the slice whose result it also pushed to the peers (PUSH).
@@ -728,7 +683,7 @@ __device__ __forceinline__ uint32_t read_fold(const CollParams& p, uint64_t coff
     // variants within 256 registers without spilling)
     constexpr int h = sizeof(T) == 2 ? 1 : 0;
     if (!nvec) {
-    } else if (n == 2) read_fold_all<T, OPC, 1, MNCCL_READ_V2 - (MNCCL_READ_V2 / 3) * h, PUSH>(p, coff, nvec, lane);
+    } else if (n == 2) read_fold_all<T, OPC, 1, 12 - 4 * h, PUSH>(p, coff, nvec, lane);
     else if (n == 3) read_fold_all<T, OPC, 2, 8 - 2 * h, PUSH>(p, coff, nvec, lane);
     else if (n <= 5) read_fold_all<T, OPC, 4, 4 - h, PUSH>(p, coff, nvec, lane);
     else read_fold_all<T, OPC, 7, 3 - h, PUSH>(p, coff, nvec, lane);
@@ -819,9 +774,6 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
   if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), rx[lane < n ? lane : 0] + 1, lane < n && lane != r, ctl))
     goto aborted;
   acquire_sys(p.sys_fence);
-  if (PUSH && VEC && MNCCL_READ_STREAM && n <= 8 && read_push_stream<T, OPC>(p, w, A, lane)) {
-    // the whole chunk went as one stream (no per-iteration message in the push form)
-  } else
   for (uint32_t j = 0; j <= iters; ++j) {
     if (j < iters) {
       // F(j): fold my chunk's slice j from the peers' send buffers, store, drain, READY

@@ -153,7 +153,8 @@ MNCCL_HD uint64_t read_slice(uint64_t chunk_bytes, int C, uint64_t slice, uint64
 // result from all n ranks' pieces.  A call takes it when its n x nslices pipelines fit one round
 // (n x nslices <= C) and its bytes (n chunks) are at most kOneShotMaxBytes -- or at any size that
 // fits when forced (MINI_NCCL_ALGO=oneshot).  Each rank sends (n - 1) x the call's bytes: a
-// latency path, not a bandwidth one.
+// latency path, not a bandwidth one.  Under auto it replaces the ring for small calls whose
+// buffers the read schedule cannot take (host memory, a full export table).
 constexpr uint64_t kOneShotMaxBytes = 64u << 10;
 MNCCL_HD uint64_t oneshot_slice(uint64_t chunk_bytes, int n, int C, uint64_t slot_bytes) {
   const int per = n > 0 && C / n > 0 ? C / n : 1;

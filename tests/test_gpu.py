@@ -151,8 +151,8 @@ def test_auto_schedule_no_init_allreduce(dev):
     assert all("error" not in out[r] for r in range(3)), out
     for r in range(3):
         i = out[r]["info"]
-        # auto (-1): one-shot for small calls, then the read schedule; its fallback for buffers
-        # that cannot be shared: the ring here
+        # auto (-1): the read schedule; its fallback for buffers that cannot be shared: the ring
+        # here (the one-shot for small ones)
         assert i["tune_ms"] == [0.0, 0.0] and i["algo"] == -1 and i["scratch_algo"] == 0, i
         assert i["read_push"] == 1 and i["calib_choice"] == -1 and i["calib_ms"] == [0.0, 0.0], i
         assert i["ranks_on_device"] == 3 and i["last_algo"] == -1, i
@@ -266,18 +266,21 @@ def test_schedules_interleaved_on_one_communicator(dev):
     n = 4
     plan = [(3, 3000), (0, 70001), (2, 1 << 18), (-1, 4096), (3, 16384), (0, 1000), (-1, 1 << 20), (2, 777),
             (3, 100003), (-1, 65536 // 4), (0, 5), (3, 8 * 1024)]
+    # (auto: device buffers every rank shares run the read schedule at every size)
     cases = [_case(count=c, algo=a, calls=2, vary=True, seed=800 + i, inplace=(i % 2 == 0),
-                   **({"expect_algo": 3} if a == -1 and c * 4 <= 64 << 10 else {})) for i, (a, c) in enumerate(plan)]
+                   **({"expect_algo": 2} if a == -1 else {})) for i, (a, c) in enumerate(plan)]
     _run_allreduce(n, cases, timeout=600)
 
 
 @pytest.mark.parametrize("mem", ["pinned", "pageable"])
 def test_oneshot_host_buffers(dev, mem):
     # auto's small calls on host buffers (the ring's domain before one-shot): pinned memory read
-    # and written through its device mapping, pageable memory staged through HBM
+    # and written through its device mapping, pageable memory staged through HBM; above 64 KiB
+    # the ring again
     cases = [_case(count=4099, algo=-1, mem=mem, seed=30, expect_algo=3),
              _case(count=3 * 5000 + 2, algo=-1, mem=mem, inplace=True, seed=31, expect_algo=3),
-             _case(dtype="bf16", count=3001, algo=-1, mem=mem, recv_mem="device", seed=32, expect_algo=3)]
+             _case(dtype="bf16", count=3001, algo=-1, mem=mem, recv_mem="device", seed=32, expect_algo=3),
+             _case(count=3 * (1 << 14) + 1, algo=-1, mem=mem, seed=33, expect_algo=0)]
     _run_allreduce(3, cases)
 
 

@@ -11,9 +11,12 @@ d = collections.defaultdict(list)
 tags = []
 tag = None
 for line in open(sys.argv[1]):
-    m = re.match(r"== (\S+) (?:round=\d+ )?n=(\d+)", line) or re.match(r"== n=(\d+) (\S+)", line)
+    m = re.match(r"== (\S+) (?:round=\d+ )?n=(\d+)", line) or re.match(r"== n=(\d+) algo=(\S+) read_push=(\d)", line)
     if m:
-        t, n = (m.group(1), m.group(2)) if not line.startswith("== n=") else (m.group(2), m.group(1))
+        if line.startswith("== n="):
+            t, n = m.group(2) + ("" if m.group(3) == "1" or m.group(2) != "read" else "_load"), m.group(1)
+        else:
+            t, n = m.group(1), m.group(2)
         tag = (t, int(n))
         if t not in tags:
             tags.append(t)

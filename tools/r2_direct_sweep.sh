@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL: the recipe of a round-2/3 profile; it sets knobs or schedules removed in 4.0 (direct,
+# PIPE_DEPTH, TUNE), so it does not run against the 4.x library.
 # Direct vs ring on the 4-rank one-GPU proxy (1 GiB fp32 per rank): which knob closes direct's
 # gap (PMC traffic is 1.007x for both, so the gap is hand-off, not bytes).  perf_test rank 0's
 # row per point; MINI_NCCL_TUNE=0.

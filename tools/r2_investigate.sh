@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL: the recipe of a round-2/3 profile; it sets knobs or schedules removed in 4.0 (direct,
+# PIPE_DEPTH, TUNE), so it does not run against the 4.x library.
 # Round-2 evidence on the one-GPU box (ranks share GPU 0):
 #  part A: 8 perf_test rank processes on one GPU (the reference's own topology,
 #          perf_test.cpp:46) under several settings; per-variant wall time, exit codes and the

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL: the recipe of a round-2/3 profile; it sets knobs or schedules removed in 4.0 (direct,
+# PIPE_DEPTH, TUNE), so it does not run against the 4.x library.
 # Read schedule (push form) vs iterations per pipeline (MINI_NCCL_PIPE_DEPTH; the default is
 # schedule.h kReadDepth = 16, chosen in round 2 for the load form's fill and drain): perf_test
 # rank 0, every rank on GPU 0 (2 HW queues each), 16 MiB / 64 MiB / 1 GiB, interleaved rounds.

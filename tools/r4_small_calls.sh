@@ -1,8 +1,10 @@
 #!/bin/bash
-# Small-call time at 2 / 4 / 8 rank processes sharing one GPU, ring and read (push form) and the
-# read schedule's load form (perf_test rank 0, 200 blocking calls per size): the round-4 library.
+# Small-call time at 2 / 4 / 8 rank processes sharing one GPU: ring, read (push form), the read
+# schedule's load form, one-shot (perf_test rank 0, ITERS blocking calls per size, ROUNDS rounds
+# interleaved), CFGS = "algo:read_push ..."; the round-4 library.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 export GPU_MAX_HW_QUEUES=${QUEUES:-2} MINI_NCCL_PERF_DEVICE=0
+for round in ${ROUNDS:-1}; do
 for nr in ${NRS:-2 4 8}; do
   for cfg in ${CFGS:-ring:1 read:1 read:0 oneshot:1}; do
     algo=${cfg%%:*}; push=${cfg#*:}
@@ -10,16 +12,17 @@ for nr in ${NRS:-2 4 8}; do
     pids=()
     for ((r = 1; r < nr; r++)); do
       MINI_NCCL_ALGO=$algo MINI_NCCL_READ_PUSH=$push MINI_NCCL_PORT=$port timeout -k 5 120 $R/apps/bin/perf_test $r $nr \
-        --sizes 4k,64k,1 --iters 200 > /tmp/sc_$r.log 2>&1 &
+        --sizes ${SIZES:-4k,64k,1} --iters ${ITERS:-200} > /tmp/sc_$r.log 2>&1 &
       pids+=($!)
     done
     MINI_NCCL_ALGO=$algo MINI_NCCL_READ_PUSH=$push MINI_NCCL_PORT=$port timeout -k 5 120 $R/apps/bin/perf_test 0 $nr \
-      --sizes 4k,64k,1 --iters 200 > /tmp/sc_0.log 2>&1
+      --sizes ${SIZES:-4k,64k,1} --iters ${ITERS:-200} > /tmp/sc_0.log 2>&1
     rc=$?
     for p in "${pids[@]}"; do wait $p; done
-    echo "== n=$nr algo=$algo read_push=$push rc=$rc"
+    echo "== n=$nr algo=$algo read_push=$push round=$round rc=$rc"
     grep -E "^ +[0-9]+ " /tmp/sc_0.log
     [ $rc -ne 0 ] && exit 9
   done
+done
 done
 exit 0
