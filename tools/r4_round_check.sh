@@ -1,0 +1,37 @@
+#!/bin/bash
+# Round-4 evidence on the one GPU, step by step (each under its own time limit; the first failure
+# ends the call): STEP=suite -> the whole -m gpu suite (one process) + smoke; STEP=n1 -> bench.py
+# N=1 and its rocprofv3 evidence (kernel trace + FETCH / WRITE passes); STEP=proxy -> the N > 1
+# bench flow with NRS rank processes sharing the GPU; STEP=small -> small calls by rank count;
+# STEP=inject -> the injected-abort rehearsal.  Outputs under gpurun_out/r4_<step>/.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+for step in ${STEP:-suite}; do
+  O=gpurun_out/r4_$step; mkdir -p $O
+  case $step in
+    suite)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 10
+      tail -2 $O/gpu_tests.log
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 11
+      tail -2 $O/smoke.log ;;
+    n1)
+      timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_n1.json 2> $O/bench_n1.err || exit 12
+      cut -c1-400 $O/bench_n1.json
+      bash tools/profile_n1.sh r4_n1/prof || exit 13 ;;
+    proxy)
+      for n in ${NRS:-2 4 8}; do
+        GPU_MAX_HW_QUEUES=2 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+          --master-addr 127.0.0.1 --master-port $((29700 + n)) bench.py --gpus $n --same-device ${BENCH_ARGS} \
+          > $O/bench_n${n}_same_gpu.json 2> $O/bench_n${n}.err || exit $((20 + n))
+        echo "n=$n"; cut -c1-300 $O/bench_n${n}_same_gpu.json
+      done ;;
+    small)
+      ROUNDS="${ROUNDS:-1 2 3}" ITERS=500 timeout -k 10 600 bash tools/r4_small_calls.sh > $O/small_calls.txt 2>&1 || exit 30
+      python3 tools/ab_summary.py $O/small_calls.txt ;;
+    inject)
+      timeout -k 10 1100 bash tools/r4_inject_check.sh > $O/inject_check.txt 2>&1 || exit 40
+      tail -12 $O/inject_check.txt ;;
+  esac
+done
+echo round-check-done
