@@ -188,6 +188,15 @@ __device__ __forceinline__ void record_timeout(const Ctl& c, const u64* flag, u6
   __hip_atomic_store(diag + 2, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// a peer's ABORT word seen: the first cause stays in the status word (a peer's abort that
+// echoes this rank's own timeout must not hide it); the word names the peer and its cause
+__device__ __forceinline__ void note_remote_abort(const Ctl& c, u64 a) {
+  if (ld_sys32(c.status) == 0) {
+    __hip_atomic_store(reinterpret_cast<u64*>(c.status + 4) + 3, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    st_sys32(c.status, kStatusRemoteAbort);
+  }
+}
+
 // lane-0 spin until *flag >= target; false on timeout / abort (status already set).  The
 // spin is out of line (kept out of the message bodies' code and registers); Ctl goes by value
 // so it travels in registers -- by reference it had to live in scratch memory.
@@ -197,13 +206,8 @@ __device__ __noinline__ bool wait_ge_spin(const u64* flag, u64 target, const Ctl
     __builtin_amdgcn_s_sleep(1);
     if (ld_sys(flag) >= target) return true;
     if ((polls & 63) == 0) {
-      // the first cause stays in the status word (a peer's abort that echoes this rank's own
-      // timeout must not hide it); the peer's ABORT word names it and its cause (abort_word)
       if (const u64 a = ld_sys(c.my_abort)) {
-        if (ld_sys32(c.status) == 0) {
-          __hip_atomic_store(reinterpret_cast<u64*>(c.status + 4) + 3, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          st_sys32(c.status, kStatusRemoteAbort);
-        }
+        note_remote_abort(c, a);
         return false;
       }
       if (ld_sys32(c.host_abort) != 0) {
@@ -259,9 +263,21 @@ __device__ __forceinline__ bool wave_wait_ge(const u64* flag, u64 target, const 
 // every peer's flag is polled in the same round instead of one peer after the other (n - 1
 // uncached round trips in a row at every hand-off of the read and one-shot kernels).  True when
 // every active lane's word arrived; a lane that gives up sets the status as wait_ge does.
-__device__ __forceinline__ bool wave_wait_peers(const u64* flag, u64 target, bool active, const Ctl& c) {
+// check_abort: lane 63 (never a peer's: at most 16 ranks) also reads this rank's ABORT word in
+// the same round -- a wait whose flags are all there already never spins, so without it a rank
+// that comes late to a call its peer gave up on (the peer raised its ABORT word, its messages
+// already sent) would complete the call as if nothing had happened.
+__device__ __forceinline__ bool wave_wait_peers(const u64* flag, u64 target, bool active, const Ctl& c, int lane,
+                                                bool check_abort) {
   int bad = 0;
-  if (active) bad = wait_ge(flag, target, c) ? 0 : 1;
+  if (active) {
+    bad = wait_ge(flag, target, c) ? 0 : 1;
+  } else if (check_abort && lane == 63) {
+    if (const u64 a = ld_sys(c.my_abort)) {
+      note_remote_abort(c, a);
+      bad = 1;
+    }
+  }
   return __builtin_amdgcn_ballot_w64(bad != 0) == 0;
 }
 
@@ -771,7 +787,8 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
   __builtin_amdgcn_wave_barrier();
   // START to every peer, then wait for theirs
   if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + 1);
-  if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), rx[lane < n ? lane : 0] + 1, lane < n && lane != r, ctl))
+  if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), rx[lane < n ? lane : 0] + 1, lane < n && lane != r, ctl, lane,
+                       true))
     goto aborted;
   acquire_sys(p.sys_fence);
   for (uint32_t j = 0; j <= iters; ++j) {
@@ -835,7 +852,8 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
     st_sys(p.peer_mbox[lane] + mbox_credit(n, C, r, w), rx[lane] + mpc);
     st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + mpc);
   }
-  if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), rx[lane < n ? lane : 0] + mpc, lane < n && lane != r, ctl))
+  if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), rx[lane < n ? lane : 0] + mpc, lane < n && lane != r, ctl, lane,
+                       false))
     goto aborted;
   if (lane < n && lane != r) {
     p.tx_seq[(u64)lane * C + w] = tx[lane] + mpc;
@@ -884,7 +902,8 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) oneshot_kernel(
   const uint32_t ne = len / (uint32_t)sizeof(T), e0 = nvec * 16 / (uint32_t)sizeof(T);
   const rsrc_t mine = make_rsrc(p.send + coff, len);
   // my message's slot in every peer must be free (the peer consumed message tx - slots)
-  if (!wave_wait_peers(p.mbox + mbox_credit(n, C, lane, w), mytx + 1 - (u64)K, peer && mytx + 1 > (u64)K, ctl))
+  if (!wave_wait_peers(p.mbox + mbox_credit(n, C, lane, w), mytx + 1 - (u64)K, peer && mytx + 1 > (u64)K, ctl, lane,
+                       false))
     goto aborted;
   // my piece into every peer's slot
   for (uint32_t i = (uint32_t)lane; i < nvec; i += 64) {
@@ -905,7 +924,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) oneshot_kernel(
   if (p.sys_fence && lane == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if (peer) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), mytx + 1);
   // every peer's piece, then the fold: in[k] = rank c + k's piece (my own send for me)
-  if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), myrx + 1, peer, ctl)) goto aborted;
+  if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), myrx + 1, peer, ctl, lane, true)) goto aborted;
   acquire_sys(p.sys_fence);
   if (len) {
     rsrc_t in[kMaxRanks];

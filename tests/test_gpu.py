@@ -130,7 +130,7 @@ def test_host_buffers(dev, algo):
     _run_allreduce(3, cases)
 
 
-@pytest.mark.parametrize("sched", SCHEDULES_ALL)
+@pytest.mark.parametrize("sched", SCHEDULES_ALL + [pytest.param((3, {}), id="oneshot")])
 @pytest.mark.parametrize("blocking", ["1", "0"], ids=["blocking", "async"])
 def test_skewed_ranks_varying_data(dev, sched, blocking):
     algo, env = sched
@@ -461,10 +461,10 @@ def test_watchdog_timeout_is_internal_error_and_sticky(dev):
     assert out[0]["async"] == M.ncclInternalError
 
 
-@pytest.mark.parametrize("algo", ["ring", "read"])
+@pytest.mark.parametrize("algo", ["ring", "read", "oneshot"])
 def test_late_peer_is_aborted_fast(dev, algo):
-    # rank 0 gives up on rank 1 (kernel watchdog for ring, the read schedule's rendezvous limit
-    # for read); either way it raises rank 1's ABORT word, so rank 1's late call fails at once
+    # rank 0 gives up on rank 1 (kernel watchdog for ring and one-shot, the read schedule's
+    # rendezvous limit for read); either way it raises rank 1's ABORT word, so rank 1's late call fails at once
     import mini_nccl as M
     port = GW.free_port()
     env = {"MINI_NCCL_TIMEOUT_MS": "1500", "STALL_SECS": "7", "LATE_CALL": "1", "MINI_NCCL_ALGO": algo}
@@ -475,7 +475,7 @@ def test_late_peer_is_aborted_fast(dev, algo):
     assert out[1]["secs"] < 1.5, out[1]  # well under its own 1.5 s watchdog + 2 s host limit
 
 
-@pytest.mark.parametrize("algo", ["ring", "read"])
+@pytest.mark.parametrize("algo", ["ring", "read", "oneshot"])
 def test_allreduce_hip_graph_capture_and_replay(dev, algo):
     # the reference only warns under capture (api.cpp:153-166); here a captured all-reduce
     # replays correctly because the FIFO counters are device state advanced by the kernel
@@ -489,10 +489,10 @@ def test_allreduce_hip_graph_capture_and_replay(dev, algo):
         assert out[r]["bad"] == [0, 0, 0, 0]
         assert out[r]["eager_rc"] == 0 and out[r]["eager_bad"] == 0
         # the read schedule is captured too (its peer mappings pinned for the replays)
-        assert out[r]["captured_algo"] == {"ring": 0, "read": 2}[algo]
+        assert out[r]["captured_algo"] == {"ring": 0, "read": 2, "oneshot": 3}[algo]
 
 
-@pytest.mark.parametrize("algo", ["ring", "read"])
+@pytest.mark.parametrize("algo", ["ring", "read", "oneshot"])
 def test_calls_on_alternating_streams_are_ordered(dev, algo):
     port = GW.free_port()
     env = {"MINI_NCCL_TIMEOUT_MS": "20000", "MINI_NCCL_ALGO": algo, "MINI_NCCL_BLOCKING": "0"}
@@ -523,7 +523,7 @@ def test_single_rank_is_copy_only(dev):
 
 
 @pytest.mark.parametrize("knob,values", [("MINI_NCCL_SLICE_SIZE", ("131072", "65536")),
-                                         ("MINI_NCCL_READ_PUSH", ("1", "0")), ("MINI_NCCL_ALGO", ("ring", "read")),
+                                         ("MINI_NCCL_READ_PUSH", ("1", "0")), ("MINI_NCCL_ALGO", ("ring", "oneshot")),
                                          ("MINI_NCCL_WINDOW_SIZE", ("64", "16"))])
 def test_mismatched_config_is_system_error(dev, knob, values):
     # every init failure is ncclSystemError, as in the reference (api.cpp:62-65)
