@@ -373,6 +373,38 @@ int main(int argc, char** argv) {
   unsigned* ticket = nullptr;
   CK(hipMalloc((void**)&ticket, 4));
   CK(hipDeviceSynchronize());
+  if (g_case && !strcmp(g_case, "alloc")) {
+    // the same kernels on 8 fresh sets of allocations, each placed behind a spacer of another
+    // size: does the rate depend on where the buffers landed (the 2-rank read kernel's bimodal
+    // 740 / 900 us at 1 GiB)?
+    for (int round = 0; round < 8; ++round) {
+      for (int k = 0; k < 4; ++k) {
+        CK(hipFree((void*)s.src[k]));
+        CK(hipFree(s.dst[k]));
+      }
+      void* spacer = nullptr;
+      const size_t sp = (size_t)((round * 37) % 251 + 1) << 20;
+      CK(hipMalloc(&spacer, sp));
+      for (int k = 0; k < 4; ++k) {
+        v4u* p = nullptr;
+        CK(hipMalloc((void**)&p, bytes));
+        CK(hipMemset(p, k + 1, bytes));
+        s.src[k] = p;
+        CK(hipMalloc((void**)&s.dst[k], bytes));
+        CK(hipMemset(s.dst[k], 0, bytes));
+      }
+      CK(hipDeviceSynchronize());
+      printf("== allocation round %d (spacer %zu MiB, src0 %p dst0 %p)\n", round, sp >> 20, (void*)s.src[0], (void*)s.dst[0]);
+      g_case = "22s";
+      run<2, 2, 17>(s, nvec, "sc0 sc1");
+      g_case = "p2";
+      run_persist2<4, false, 17>(s, nvec, 512);
+      run_persist2<4, true, 17>(s, nvec, 512);
+      g_case = "alloc";
+      CK(hipFree(spacer));
+    }
+    return 0;
+  }
   for (int rep = 0; rep < 2; ++rep) {
     run<1, 1, 2>(s, nvec, "nt");
     run<1, 1, 17>(s, nvec, "sc0 sc1");
