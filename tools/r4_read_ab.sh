@@ -2,11 +2,11 @@
 # Interleaved A/B/... of the read schedule between library builds on ONE GPU (every rank on GPU 0,
 # $QUEUES HW queues each, default 2): LIBS = "tag:dir ..." where dir holds a libmini_nccl.so
 # (LD_LIBRARY_PATH wins over the apps' RUNPATH) or is "in-tree"; perf_test rank 0 (bytes, us,
-# algbw, busbw, schedule), MINI_NCCL_ALGO=read.
+# algbw, busbw, schedule), MINI_NCCL_ALGO=$ALGO (default read).
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 LIBS=${LIBS:-"in-tree:in-tree stream:$R/tools/variants/stream"}
 SIZES=${SIZES:-64,1024}
-export GPU_MAX_HW_QUEUES=${QUEUES:-2} MINI_NCCL_PERF_DEVICE=0 MINI_NCCL_ALGO=read
+export GPU_MAX_HW_QUEUES=${QUEUES:-2} MINI_NCCL_PERF_DEVICE=0 MINI_NCCL_ALGO=${ALGO:-read}
 run() {
   local nr="$1" tag="$2"; shift 2
   local port=$((20000 + RANDOM % 20000))
