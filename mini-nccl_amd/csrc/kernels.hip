@@ -200,10 +200,13 @@ __device__ __forceinline__ void note_remote_abort(const Ctl& c, u64 a) {
 // lane-0 spin until *flag >= target; false on timeout / abort (status already set).  The
 // spin is out of line (kept out of the message bodies' code and registers); Ctl goes by value
 // so it travels in registers -- by reference it had to live in scratch memory.
+#ifndef MNCCL_POLL_SLEEP
+#define MNCCL_POLL_SLEEP 1  // s_sleep units (64 clocks each) between two polls of a flag
+#endif
 __device__ __noinline__ bool wait_ge_spin(const u64* flag, u64 target, const Ctl c) {
   const u64 t0 = __builtin_amdgcn_s_memrealtime();
   for (uint32_t polls = 1;; ++polls) {
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(MNCCL_POLL_SLEEP);
     if (ld_sys(flag) >= target) return true;
     if ((polls & 63) == 0) {
       if (const u64 a = ld_sys(c.my_abort)) {
