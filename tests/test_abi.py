@@ -172,6 +172,9 @@ def test_config_from_env(sim_lib, monkeypatch):
     monkeypatch.setenv("MINI_NCCL_ALGO", "auto")
     rc, s = S.config_describe()
     assert rc == 0 and "algo=auto" in s
+    monkeypatch.setenv("MINI_NCCL_ALGO", "oneshot")      # 4.1
+    rc, s = S.config_describe()
+    assert rc == 0 and "algo=oneshot" in s
     monkeypatch.setenv("MINI_NCCL_ALGO", "tree")
     rc, s = S.config_describe()
     assert rc == -1 and "MINI_NCCL_ALGO" in s
