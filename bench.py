@@ -363,6 +363,43 @@ def size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks, 
     return rows
 
 
+def small_calls(M, torch, dist, comm, send, recv, stream, n, max_over_ranks, warm=10, reps=100):
+    """us per blocking 4 KiB / 64 KiB fp32 call for each schedule (forced), all ranks in step:
+    what auto's order for small calls (read first for shareable device buffers, the one-shot for
+    the ring's small calls) should be decided from on this topology"""
+    rows = []
+    names = {"ring": M.ALGO_RING, "read": M.ALGO_READ, "oneshot": M.ALGO_ONESHOT}
+    try:
+        for kib in (4, 64):
+            k = (kib << 10) // 4
+            s_, r_ = send[:k], recv[:k]
+            row = {"KiB": kib}
+            for name, a in names.items():
+                comm.set_algo(a)
+
+                def call():
+                    rc = comm.all_reduce(s_.data_ptr(), r_.data_ptr(), k, M.ncclFloat, M.ncclSum, stream.cuda_stream)
+                    if rc != 0:
+                        raise M.NcclError(rc, f"ncclAllReduce ({name}, {kib} KiB)")
+                for _ in range(warm):
+                    call()
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    call()
+                    torch.cuda.synchronize()
+                dt = max_over_ranks(time.perf_counter() - t0) / reps
+                ran = comm.info()["last_algo"]
+                row[name + "_us"] = round(dt * 1e6, 1)
+                row[name + "_ok"] = max_over_ranks(0.0 if (ran == a and bool((r_ == float(n)).all().item()))
+                                                   else 1.0) == 0.0
+            rows.append(row)
+    finally:
+        comm.set_algo(M.ALGO_AUTO)
+    return rows
+
+
 def host_buffer_rate(M, torch, dist, comm, stream, n, max_over_ranks, mib=256, warm=2, reps=5):
     """algbw of ncclAllReduce on pinned host send/recv buffers (never the headline value)"""
     err = None
@@ -745,7 +782,7 @@ def main():
         def inject(where):
             """MNCCL_BENCH_INJECT=<where>: rehearses the failure paths below (a GPU fault aborts the
             process: the armed line must still come out).  Stages after the ring: run_read (the
-            headline), probe, standalone, rccl, sizes, host_buffers, sweep; <stage>_error raises
+            headline), probe, standalone, rccl, sizes, small_calls, host_buffers, sweep; <stage>_error raises
             an ncclInternalError there instead"""
             if os.environ.get("MNCCL_BENCH_INJECT") == where and rank == 0:
                 log(f"injected abort at {where}")
@@ -1083,6 +1120,17 @@ def main():
             result["sizes"] = {"error": str(e)[:200]}
         if rank == 0:
             arm(result)
+        # small calls by schedule (the one-shot's place in auto is to be re-decided per topology)
+        if args.dtype == "f32":
+            if rank == 0:
+                log("extras: small calls")
+            try:
+                inject("small_calls")
+                result["small_calls"] = small_calls(M, torch, dist, comm, send, recv, stream, n, max_over_ranks)
+            except Exception as e:
+                result["small_calls"] = {"error": str(e)[:200]}
+            if rank == 0:
+                arm(result)
         # the reference's own usage: host buffers in, host buffers out (perf_test.cpp:78-79);
         # pinned memory is mapped into the kernel, so this is the PCIe-inclusive end-to-end rate
         if args.dtype == "f32":

@@ -7,7 +7,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R; mkdir -p gpurun_out/inject
 port=29810
-for stage in ${STAGES:-run_read probe standalone rccl sizes host_buffers sweep}; do
+for stage in ${STAGES:-run_read probe standalone rccl sizes small_calls host_buffers sweep}; do
   port=$((port + 1))
   args="--no-sweep"
   [ $stage = sweep ] && args=""
@@ -26,7 +26,7 @@ d = json.loads(lines[0])
 sch = {k: v.get("value", v.get("error", "?")) for k, v in d.get("schedules", {}).items()}
 print(f"{stage}: rc={rc} one line, value={d.get('value')} result_check={d.get('config', {}).get('result_check', '-')[:60]!r} "
       f"schedules={sch} roofline.frac={d.get('roofline', {}).get('frac')} cpu_baseline={'yes' if d.get('cpu_baseline') else 'no'} "
-      f"extras={[k for k in ('link', 'rccl_reference', 'sizes', 'host_buffers', 'sweep') if k in d]}")
+      f"extras={[k for k in ('link', 'rccl_reference', 'sizes', 'small_calls', 'host_buffers', 'sweep') if k in d]}")
 EOF
 done
 echo inject-check-done
