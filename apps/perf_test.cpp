@@ -157,7 +157,7 @@ int main(int argc, char** argv) {
     mncclCommInfo_t info;
     memset(&info, 0, sizeof info);
     const char* sched = !mncclCommGetInfoV || mncclCommGetInfoV(comm, &info, sizeof info) != ncclSuccess ? "?"
-                        : info.last_algo == 0 ? "ring" : info.last_algo == 1 ? "direct" : info.last_algo == 2 ? "read" : "-";
+                        : info.last_algo == 0 ? "ring" : info.last_algo == 2 ? "read" : info.last_algo == 3 ? "oneshot" : "-";
     if (rank == 0) printf("%15zu %15.2f %15.2f %15.2f %9s %s\n", bytes, us, alg, bus, sched, bad >= 0 ? "(FAIL)" : "");
     fflush(stdout);
     HIP_OK(hipFree(d_send));
