@@ -1,6 +1,6 @@
 """Resource budget of the shipped gfx950 kernels, read from the built library (CPU only).
 
-The persistent collective kernels (ring / direct / read) of every rank must be resident on the
+The collective kernels (ring / read / one-shot) of every rank must be resident on the
 GPU at the same time: each waits for its peers' kernels.  With 8 rank processes sharing one GPU
 (the reference's perf_test topology) that is 8 x 256 one-wave pipelines = 2 waves on each of
 the 1024 SIMDs, so no collective kernel may use more than 256 registers per lane (VGPRs +
@@ -60,9 +60,9 @@ def _kernels(tmp_path):
 @pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(READELF)), reason="library not built / no llvm-readelf")
 def test_collective_kernels_fit_two_waves_per_simd_without_scratch(tmp_path):
     ks = _kernels(tmp_path)
-    coll = {k: v for k, v in ks.items() if re.search(r"(ring|direct|read)_kernel", k)}
-    # 3 schedules x 5 dtypes x 4 ops x (vector, scalar) instantiations
-    assert len(coll) == 120, sorted(coll)[:5]
+    coll = {k: v for k, v in ks.items() if re.search(r"(ring|read|oneshot)_kernel", k)}
+    # (ring, read push form, read load form, one-shot) x 5 dtypes x 4 ops x (vector, scalar)
+    assert len(coll) == 160, sorted(coll)[:5]
     over = {k: v for k, v in coll.items() if v["vgpr_count"] + v["agpr_count"] > 256}
     assert not over, f"collective kernels above 256 registers (1 wave per SIMD): {over}"
     spill = {k: v for k, v in ks.items() if v["private_segment_fixed_size"] != 0}
