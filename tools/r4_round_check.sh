@@ -3,7 +3,8 @@
 # ends the call): STEP=suite -> the whole -m gpu suite (one process) + smoke; STEP=n1 -> bench.py
 # N=1 and its rocprofv3 evidence (kernel trace + FETCH / WRITE passes); STEP=proxy -> the N > 1
 # bench flow with NRS rank processes sharing the GPU; STEP=small -> small calls by rank count;
-# STEP=inject -> the injected-abort rehearsal.  Outputs under gpurun_out/r4_<step>/.
+# STEP=stress -> the mixed-schedule stress at 8 and 3 ranks; STEP=inject -> the injected-abort
+# rehearsal.  Outputs under gpurun_out/r4_<step>/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
@@ -29,6 +30,10 @@ for step in ${STEP:-suite}; do
     small)
       ROUNDS="${ROUNDS:-1 2 3}" ITERS=500 timeout -k 10 600 bash tools/r4_small_calls.sh > $O/small_calls.txt 2>&1 || exit 30
       python3 tools/ab_summary.py $O/small_calls.txt ;;
+    stress)
+      timeout -k 10 550 python -u tools/r4_stress_mixed.py --ranks 8 --calls 200 --seed 11 > $O/stress_n8.txt 2>&1 || exit 50
+      timeout -k 10 400 python -u tools/r4_stress_mixed.py --ranks 3 --calls 200 --seed 12 > $O/stress_n3.txt 2>&1 || exit 51
+      grep STRESS $O/stress_n8.txt $O/stress_n3.txt ;;
     inject)
       timeout -k 10 1100 bash tools/r4_inject_check.sh > $O/inject_check.txt 2>&1 || exit 40
       tail -12 $O/inject_check.txt ;;
