@@ -373,6 +373,36 @@ int main(int argc, char** argv) {
   unsigned* ticket = nullptr;
   CK(hipMalloc((void**)&ticket, 4));
   CK(hipDeviceSynchronize());
+  if (g_case && !strcmp(g_case, "offset")) {
+    // one allocation; stream k (src0, src1, dst0, dst1) at k x (bytes + delta): the same physical
+    // pages for every delta, only the streams' relative offsets change -- does the persistent
+    // form's rate follow the relative placement of its streams?
+    for (int k = 0; k < 4; ++k) {
+      CK(hipFree((void*)s.src[k]));
+      CK(hipFree(s.dst[k]));
+    }
+    char* big = nullptr;
+    const size_t slack = 64ull << 20;
+    CK(hipMalloc((void**)&big, 4 * (bytes + slack)));
+    CK(hipMemset(big, 1, 4 * (bytes + slack)));
+    const size_t deltas[] = {0, 4096, 65536, 256 << 10, 1 << 20, (2 << 20) + 65536, 8 << 20, (32 << 20) + 4096};
+    for (size_t d : deltas) {
+      Streams t;
+      t.src[0] = (const v4u*)(big + 0 * (bytes + d));
+      t.src[1] = (const v4u*)(big + 1 * (bytes + d));
+      t.dst[0] = (v4u*)(big + 2 * (bytes + d));
+      t.dst[1] = (v4u*)(big + 3 * (bytes + d));
+      t.src[2] = t.src[3] = t.src[0];
+      t.dst[2] = t.dst[3] = t.dst[0];
+      printf("== delta %zu B\n", d);
+      g_case = "22s";
+      run<2, 2, 17>(t, nvec, "sc0 sc1");
+      g_case = "p2";
+      run_persist2<4, false, 17>(t, nvec, 512);
+      run_persist2<12, true, 17>(t, nvec, 512);
+    }
+    return 0;
+  }
   if (g_case && !strcmp(g_case, "alloc")) {
     // the same kernels on 8 fresh sets of allocations, each placed behind a spacer of another
     // size: does the rate depend on where the buffers landed (the 2-rank read kernel's bimodal
