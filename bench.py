@@ -790,6 +790,8 @@ def main():
             if os.environ.get("MNCCL_BENCH_INJECT") == where + "_error":
                 raise M.NcclError(M.ncclInternalError, f"injected at {where} (MNCCL_BENCH_INJECT)")
 
+        fallbacks = {}
+
         def run_algo(algo, auto=False):
             comm.set_algo(M.ALGO_AUTO if auto else ALGO_IDS[algo])
             inject(f"run_{algo}")
@@ -806,7 +808,16 @@ def main():
             ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream,
                                     barrier=dist.barrier)
             i = comm.info()
-            ok = ok and i["last_algo"] == ALGO_IDS[algo]  # the timed calls ran this schedule (no fallback)
+            ran_ok = i["last_algo"] == ALGO_IDS[algo]  # the timed calls ran this schedule (no fallback)
+            if not ran_ok:
+                # e.g. the read schedule could not map a peer's buffers on this node and the calls
+                # ran the ring: on record in the line, not only as a FAILED check
+                fallbacks[algo] = {"rank": rank, "ran": {0: "ring", 2: "read", 3: "oneshot"}.get(i["last_algo"], "?"),
+                                   "read_map_failures": i["read_map_failures"],
+                                   "ipc_open_failures": i["ipc_open_failures"], "cap_refusals": i["cap_refusals"]}
+                log(f"rank {rank}: {algo} calls ran {fallbacks[algo]['ran']}: {fallbacks[algo]}")
+                result["config"]["fallbacks"] = dict(fallbacks)
+            ok = ok and ran_ok
             send.fill_(1.0)
             ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
             return max_over_ranks(wall), max_over_ranks(ev_ms), ok
@@ -854,6 +865,8 @@ def main():
             })
             if note:
                 result["config"]["result_check"] = note
+            if fallbacks:
+                result["config"]["fallbacks"] = dict(fallbacks)
             return bw
 
         headline_why = ("the library default for device buffers (MINI_NCCL_ALGO=auto -> read: each rank folds its "
