@@ -44,6 +44,7 @@ __global__ void __launch_bounds__(64) mix2(Streams s, unsigned long long nvec) {
 }
 
 static const char* g_case = nullptr;
+static bool g_mode_geo = false;  // "allocgeo": the alloc rounds with the persistent geometry sweep
 
 // The read kernel's structure without its protocol (read_fold_all at n = 2: one peer stream and
 // the local stream read, the result stored twice, V vectors per lane per batch, the next batch's
@@ -360,6 +361,10 @@ int main(int argc, char** argv) {
   const unsigned long long mib = argc > 1 ? strtoull(argv[1], nullptr, 0) : 512;
   const unsigned long long bytes = mib << 20, nvec = bytes / 16;
   if (argc > 2) g_case = argv[2];
+  if (g_case && !strcmp(g_case, "allocgeo")) {
+    g_case = "alloc";
+    g_mode_geo = true;
+  }
   CK(hipSetDevice(0));
   Streams s;
   for (int k = 0; k < 4; ++k) {
@@ -430,6 +435,15 @@ int main(int argc, char** argv) {
       g_case = "p2";
       run_persist2<4, false, 17>(s, nvec, 512);
       run_persist2<4, true, 17>(s, nvec, 512);
+      if (g_mode_geo) {  // which persistent geometry holds its rate on every placement?
+        run_persist2<1, false, 17>(s, nvec, 1024);
+        run_persist2<1, false, 17>(s, nvec, 2048);
+        run_persist2<2, false, 17>(s, nvec, 512);
+        run_persist2<2, false, 17>(s, nvec, 1024);
+        run_persist2<4, false, 17>(s, nvec, 256);
+        run_persist2<4, false, 17>(s, nvec, 1024);
+        run_persist2<12, true, 17>(s, nvec, 512);
+      }
       g_case = "alloc";
       CK(hipFree(spacer));
     }
