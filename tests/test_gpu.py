@@ -259,6 +259,21 @@ def test_oneshot_parity(dev, n):
     _run_allreduce(n, cases, timeout=600)
 
 
+def test_oneshot_10_ranks(dev):
+    # past a node's 8 ranks (up to 16 per communicator): the one-shot's per-peer lanes and pieces
+    # beyond 8, interleaved with ring and read calls; 10 rank processes on the one GPU with 64
+    # pipelines and one hardware queue each (all resident at once), bit-exact vs the oracle
+    cases = [_case(count=10 * 997 + 3, algo=3, seed=40),
+             _case(dtype="bf16", count=10 * 3001, algo=3, seed=41, inplace=True),
+             _case(op="max", count=10 * 512 + 9, algo=3, seed=42, special=True),
+             _case(count=10 * 70001, algo=0, seed=43),
+             _case(count=4099, algo=-1, seed=44, mem="pinned", expect_algo=3),
+             _case(count=10 * 5000, algo=2, seed=45, calls=2, vary=True),
+             _case(count=12345, algo=3, seed=46, calls=3, vary=True)]
+    env = {"MINI_NCCL_CHANNELS": "64", "GPU_MAX_HW_QUEUES": "1"}
+    _run_allreduce(10, cases, env, timeout=600)
+
+
 def test_schedules_interleaved_on_one_communicator(dev):
     # the one-shot, the ring and the read schedule share the per-(pair, pipeline) FIFO counters,
     # READY words, credits and scratch slots: calls of all three (and auto's choice by size)
