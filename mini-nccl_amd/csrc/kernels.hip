@@ -11,6 +11,9 @@
 //  read_kernel    the default: same association order, no scratch -- each rank loads its
 //                 peers' send buffers over the links and pushes its results into their recv
 //                 buffers (mapped by Comm per allocation).
+//  oneshot_kernel small calls the read schedule cannot take (host buffers): one hand-off -- every
+//                 rank stores its pieces into every peer's scratch and folds the result itself,
+//                 same association order.
 //  local_reduce   the element-wise op alone: out = op(local, incoming), 16 B per lane.
 //
 // Memory-ordering protocol (cross-process, cross-device over xGMI):

@@ -20,6 +20,10 @@
 // its own chunk r straight from the peers' send buffers in ring order r, r+1, ..., r-1
 // (acc = op(x_q, acc): the visited rank's value is the LEFT/local operand exactly as at rank q
 // of the ring) and pushes the result into every peer's recv (kernels.hip read_kernel).
+//
+// One-shot (small calls the read schedule cannot take): every rank stores its pieces into every
+// peer's scratch and folds each piece of the result from all n ranks in that same order
+// (kernels.hip oneshot_kernel; geometry below).
 #pragma once
 #include <stdint.h>
 
