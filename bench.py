@@ -69,7 +69,16 @@ def cpu_baseline(budget_s=18.0):
         iters += k
     t_mt = spent / iters
     t_st = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, 1, 1)
-    ok = L.oracle_verify_avx2(a.ctypes.data, COUNT, float(1.0 + 2.0 * (2 + iters))) == -1
+    # every core the lease allows (affinity, bounded by the cgroup's CPU quota), beside the
+    # 16-thread figure: a few passes, same workload
+    lease = lease_cores()
+    t_all, all_iters = None, 0
+    if lease > threads:
+        t_all = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, lease, 1)  # warm
+        all_iters = max(1, min(200, int(3.0 / max(t_all, 1e-3))))
+        t_all = L.oracle_cpu_local_reduce_avx2(a.ctypes.data, b.ctypes.data, COUNT, lease, all_iters)
+    ok = L.oracle_verify_avx2(a.ctypes.data, COUNT,
+                              float(1.0 + 2.0 * (2 + iters + (1 + all_iters if t_all else 0)))) == -1
     del a, b
     # C1: 2 ranks over loopback TCP, 4 MiB fp32, 128 KiB slices (BASELINE.json configs[0])
     c1 = None
@@ -115,31 +124,57 @@ def cpu_baseline(budget_s=18.0):
         "sample": f"a += b over the full 1 GiB fp32 workload, {iters} timed passes after 1 warm pass "
                   f"(AVX2 _mm256_add_ps, {threads} threads); verify scan {'ok' if ok else 'FAILED'}",
         "single_thread_GBps": round(COUNT * 4 / t_st / 1e9, 3),
+        "lease_cores": lease,
+        "lease_GBps": round(COUNT * 4 / t_all / 1e9, 3) if t_all else None,
+        "lease_note": (f"the same 1 GiB a += b on all {lease} cores the lease allows, {all_iters} passes"
+                       if t_all else f"the lease allows {lease} cores: the {threads}-thread figure is all of them"),
         "nproc": os.cpu_count(),  # the whole machine's CPUs (the box's share is 16)
         "c1_tcp_ring": c1,
         "wall_s": round(time.time() - t_start, 1),
     }
 
 
-def cpu_ring_baseline(n, budget_s=4.0):
+def lease_cores():
+    """CPUs this process may run on: its affinity, bounded by the cgroup's CPU quota (the GPU box
+    gives a one-GPU lease 16 of the machine's cores)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_ring_baseline(n, budget_s=6.0):
     """N > 1 companion of cpu_baseline: the host ring, n threads of this box
-    (one per rank), the reference's schedule and operand order with AVX2 adds, on a bounded
-    sample (256 MiB fp32 per rank, not the 1 GiB of the GPU runs)."""
+    (one per rank), the reference's schedule and operand order with AVX2 adds, on the workload's
+    own size (1 GiB fp32 per rank, as the GPU runs)."""
     import ctypes
 
     import numpy as np
 
     import oracle_api as O
     L = O.load()
-    cnt = (256 << 20) // 4
+    cnt = COUNT
     bufs = [np.ones(cnt, np.float32) for _ in range(n)]
     arr = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
     t1 = L.oracle_cpu_ring_threads_avx2(arr, n, cnt, 131072, 1)  # also the first touch
     iters = max(1, min(10, int(budget_s / max(t1, 1e-3))))
     t = L.oracle_cpu_ring_threads_avx2(arr, n, cnt, 131072, iters)
+    # the known answer (perf_test.cpp:81-134): one more call on fresh all-ones gives n everywhere
+    for b in bufs:
+        b.fill(1.0)
+    L.oracle_cpu_ring_threads_avx2(arr, n, cnt, 131072, 1)
+    ok = all(L.oracle_verify_avx2(b.ctypes.data, (cnt // n) * n, float(n)) == -1 for b in bufs)
+    del bufs
     return {"value": round(cnt * 4 / t / 1e9, 3), "unit": "GB/s", "cores": n, "nproc": os.cpu_count(), "kind": "port",
-            "sample": f"{n}-thread in-process host ring (reference schedule, AVX2 adds), 256 MiB fp32 per rank, "
-                      f"{iters} timed all-reduces after 1"}
+            "sample": f"{n}-thread in-process host ring (reference schedule, AVX2 adds), 1 GiB fp32 per rank (the "
+                      f"workload's size), {iters} timed all-reduces after 1; known answer {'ok' if ok else 'FAILED'}"}
 
 
 # ------------------------------------------------------------------ N > 1 configuration sweeps
@@ -267,6 +302,65 @@ def verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stre
             ok = bool(torch.equal(recv[a:b].float(), exp))
             del exp
     return ok
+
+
+def order_ranges(count, n, piece=1 << 24):
+    """The pieces verify_order generates and checks, in increasing order: chunk by chunk (so a
+    piece never straddles two chunks), then the count % n tail."""
+    chunk = count // n
+    for c in range(n):
+        for a in range(c * chunk, (c + 1) * chunk, piece):
+            yield c, a, min((c + 1) * chunk, a + piece)
+    if chunk * n < count:
+        yield -1, chunk * n, count
+
+
+def verify_order(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream, barrier, seed=1234):
+    """one call on seeded uniform[-1, 1) inputs (rank q's from seed 1234 + q,
+    SURVEY.md s8(d)), every element of the result compared bit for bit with the reference ring's
+    association: the reduce of chunk c starts at rank c and visits c+1, ..., c-1, each adding its
+    own value as the local operand (mini_nccl.cu:108-126), i.e. x[c-1] + (... + (x[c+1] + x[c])).
+    Each rank regenerates every peer's input on its own GPU, piece by piece (the same generator
+    stream the peer filled its send buffer with), and folds with torch's own adds -- torch, not the
+    oracle, so the check is outside the timed path and the oracle rule.  Unlike verify_calls'
+    integer-valued data, a wrong association changes bits here.  Returns "ok" or what differed."""
+    chunk = count // n
+    ity = torch.int32 if tdt == torch.float32 else torch.int16
+
+    def gen(q):
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + q)
+        return g
+
+    def draw(g, m):
+        return (torch.rand(m, generator=g, device=dev, dtype=torch.float32) * 2 - 1).to(tdt)
+
+    g = gen(rank)
+    for _, a, b in order_ranges(count, n):
+        send[a:b].copy_(draw(g, b - a))
+    recv.fill_(-1)
+    torch.cuda.synchronize()
+    barrier()
+    rc = comm.all_reduce(send.data_ptr(), recv.data_ptr(), count, ndt, M.ncclSum, stream.cuda_stream)
+    torch.cuda.synchronize()
+    if rc != 0 or comm.async_error() != 0:
+        return f"FAILED: ncclAllReduce returned {rc} (async {comm.async_error()})"
+    gens = [gen(q) for q in range(n)]
+    for c, a, b in order_ranges(count, n):
+        xs = [draw(gens[q], b - a) for q in range(n)]
+        if c < 0:  # the count % n tail keeps this rank's own input (mini_nccl.cu:69)
+            want = xs[rank]
+        else:
+            want = xs[c]
+            for k in range(1, n):
+                want = xs[(c + k) % n] + want
+        got = recv[a:b]
+        if not torch.equal(got.view(ity), want.view(ity)):
+            i = int(torch.nonzero(got.view(ity) != want.view(ity))[0].item())
+            return (f"FAILED: element {a + i} (chunk {c}) is {got[i].item()!r}, the ring's association gives "
+                    f"{want[i].item()!r}")
+        del xs, want
+    return "ok"
 
 
 def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_point=lambda: None):
@@ -765,7 +859,9 @@ def main():
         # --algo forces one schedule
         auto_mode = args.algo == "auto"
         if auto_mode:
-            args.algo = "read" if info["algo"] < 0 else ALGO_NAMES[info["algo"]]
+            # auto: read where the topology rule allows it on every pair of ranks, else the ring
+            # (schedule.h topology_blocks_read; the library decides, the line reports)
+            args.algo = ("read" if info["auto_read"] else "ring") if info["algo"] < 0 else ALGO_NAMES[info["algo"]]
         headline_algo = args.algo
         send = torch.ones(count, device=dev, dtype=tdt)
         recv = torch.empty(count, device=dev, dtype=tdt)
@@ -791,6 +887,7 @@ def main():
                 raise M.NcclError(M.ncclInternalError, f"injected at {where} (MNCCL_BENCH_INJECT)")
 
         fallbacks = {}
+        verifies = {}
 
         def run_algo(algo, auto=False):
             comm.set_algo(M.ALGO_AUTO if auto else ALGO_IDS[algo])
@@ -807,6 +904,17 @@ def main():
             # then 3 calls on varying data (outside the timed region), restoring the buffers
             ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream,
                                     barrier=dist.barrier)
+            # and one call on seeded uniform data against the ring's association, every element
+            order = verify_order(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stream, dist.barrier)
+            bad_order = max_over_ranks(0.0 if order == "ok" else 1.0 + rank)
+            verifies[algo] = {"order_sensitive": "ok" if bad_order == 0.0 else
+                              (order if order != "ok" else f"FAILED on rank {int(bad_order) - 1}"),
+                              "what": "seeded uniform[-1, 1) inputs (seed 1234 + rank), every element of every "
+                                      "rank vs torch fp32 adds in the ring's association x[c-1] + (... + "
+                                      "(x[c+1] + x[c])), bit for bit",
+                              "integer_calls": "3 calls of rank- and position-dependent integer data, every "
+                                               "element" + ("" if ok else ": FAILED")}
+            ok = ok and order == "ok"
             i = comm.info()
             ran_ok = i["last_algo"] == ALGO_IDS[algo]  # the timed calls ran this schedule (no fallback)
             if not ran_ok:
@@ -830,6 +938,7 @@ def main():
             return {"algo": algo, "kernel_form": kernel_form(algo, info["read_push"]),
                     "value": round(nbytes / (ms_ / 1e3) / 1e9, 3), "ms_per_step": round(ms_, 4),
                     "kernel_ms": round(ev_ms, 4), "result_check": "ok" if ok else "FAILED",
+                    "verify": verifies.get(algo),
                     "roofline": {"frac": round(sum_bytes / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                                  "fused_frac": round(fused / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                                  "fused_alg_bytes_per_launch": fused}}
@@ -851,7 +960,12 @@ def main():
                            "pipelines": info["pipelines"], "scratch_bytes": info["scratch_bytes"],
                            "ranks_on_device": info["ranks_on_device"],
                            "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
-                           "read_push": info["read_push"], "headline_schedule": headline_why},
+                           "read_push": info["read_push"], "headline_schedule": headline_why,
+                           "auto_schedule": {"read": bool(info["auto_read"]), "reason": info["auto_reason"],
+                                             "rank0_peer_link": info["peer_link"],
+                                             "rank0_peer_hops": info["peer_hops"],
+                                             "rule": "auto runs read only if every pair of ranks shares a GPU or "
+                                                     "is one xGMI hop apart (csrc/schedule.h topology_blocks_read)"}},
                 "roofline": {"bound": "hbm", "achieved": round(sum_bytes / (ev_ms / 1e3) / 1e9, 2),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(sum_bytes / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),

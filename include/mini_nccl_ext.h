@@ -31,13 +31,18 @@ extern "C" {
    MINI_NCCL_TUNE removed; 400 the direct schedule and MINI_NCCL_PULL / DIRECT_OVERLAP /
    CALIBRATE / PIPE_DEPTH / MIN_SLICE / STAGE_HOST removed, MINI_NCCL_READ_PUSH added, the ring
    runs only the pipelines a call's slices need, mncclCommInfo_t grew again (same prefix);
-   401 the one-shot schedule (mncclAlgoOneShot; auto's small calls that would run the ring) */
-#define MNCCL_VERSION 401
+   401 the one-shot schedule (mncclAlgoOneShot; auto's small calls that would run the ring);
+   500 auto runs the read schedule only where every pair of GPUs is one xGMI hop apart (or
+   shares a GPU), mncclCommInfo_t grew (same prefix: auto_read, peer_link / peer_hops,
+   auto_reason) */
+#define MNCCL_VERSION 500
 
 /* schedules; all produce bit-identical results (same fold order per element) */
 typedef enum {
-  mncclAlgoAuto = -1,  /* the library's default: read for device buffers every rank can share;
-                          every other call one-shot when at most 64 KiB, else the ring */
+  mncclAlgoAuto = -1,  /* the library's default: read for device buffers every rank can share
+                          when every pair of GPUs is one xGMI hop apart (or shares a GPU: see
+                          mncclCommInfo_t.auto_read); every other call one-shot when at most
+                          64 KiB, else the ring */
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
   mncclAlgoDirect = 1, /* removed in 400 (never faster than the ring); mncclCommSetAlgo and
                           MINI_NCCL_ALGO reject it */
@@ -102,6 +107,15 @@ typedef struct {
                                             exports (per call: the call's own buffers + at most
                                             4 others) */
   int read_push;                         /* MINI_NCCL_READ_PUSH: 1 push form, 0 load form */
+  /* since 500 */
+  int auto_read;                         /* 1: the topology lets auto run the read schedule (every pair
+                                            of ranks shares a GPU or is one xGMI hop apart; the
+                                            same on every rank); 0: auto runs the ring */
+  int peer_link[16];                     /* how this rank's GPU reaches rank q's: -1 the same GPU,
+                                            -2 unknown (not visible here), else the runtime's link
+                                            type (hipExtGetLinkTypeAndHopCount: 2 PCIe, 4 xGMI) */
+  int peer_hops[16];                     /* hop count of that link (0 for the same GPU) */
+  char auto_reason[160];                 /* the rule's verdict in words (NUL-terminated) */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,

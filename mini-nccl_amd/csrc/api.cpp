@@ -186,6 +186,12 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
   info->cap_refusals = mnccl::ipc::cap_refusals();
   info->liveness_queries = mnccl::ipc::liveness_queries();
   info->read_push = k.read_push;
+  info->auto_read = c->topology_allows_read() ? 1 : 0;
+  for (int q = 0; q < 16; ++q) {
+    info->peer_link[q] = q < c->nranks() ? c->peer_link(q) : -1;
+    info->peer_hops[q] = q < c->nranks() ? c->peer_hops(q) : 0;
+  }
+  snprintf(info->auto_reason, sizeof info->auto_reason, "%s", c->topology_reason().c_str());
   memcpy(out, &full, size < sizeof full ? size : sizeof full);
   return ncclSuccess;
 }

@@ -146,14 +146,16 @@ void Comm::setup_device_resources() {
     scratch_ = (char*)ipc::pool_acquire(scratch_bytes_, hipDeviceMallocUncached, &scratch_h_, &scratch_id_);
     mbox_ = (uint64_t*)ipc::pool_acquire(mbox_bytes_, hipDeviceMallocUncached, &mbox_h_, &mbox_id_);
     const size_t seq_bytes = (size_t)2 * nranks_ * C * sizeof(uint64_t);  // C = wave channels
-    hip_check(hipMalloc((void**)&pair_seq_, seq_bytes), "alloc pair_seq");
+    // + the kernels' claim word (kernels.h CollParams::claim) in its own 256 bytes after them
+    hip_check(hipMalloc((void**)&pair_seq_, seq_bytes + 256), "alloc pair_seq");
+    claim_ = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(pair_seq_) + seq_bytes);
     // zeroed on a private stream: a device-wide sync (or the legacy null stream) would also wait
     // for other communicators' persistent kernels in this process, which may be waiting for us
     hipStream_t st = nullptr;
     hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "init stream");
     hipError_t e = hipMemsetAsync(scratch_, 0, scratch_bytes_, st);
     if (e == hipSuccess) e = hipMemsetAsync(mbox_, 0, mbox_bytes_, st);
-    if (e == hipSuccess) e = hipMemsetAsync(pair_seq_, 0, seq_bytes, st);
+    if (e == hipSuccess) e = hipMemsetAsync(pair_seq_, 0, seq_bytes + 256, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     hipStreamDestroy(st);
     hip_check(e, "zero scratch / mailbox / counters");
@@ -233,6 +235,7 @@ void Comm::exchange_and_map() {
               "(and no other process using this GPU), or calls will stall on time-slicing\n",
               procs.size(), device_, queues);
   }
+  classify_topology(all.data());
   for (int q = 0; q < nranks_; ++q) {
     if (q == rank_) {
       peer_scratch_[(size_t)q] = scratch_;
@@ -279,6 +282,63 @@ void Comm::exchange_and_map() {
   registered_ = true;
 }
 
+// How this rank's GPU reaches every peer's (the runtime's link type and hop count), gathered from
+// every rank; auto runs the read schedule only if schedule.h topology_blocks_read allows it for
+// every pair -- the same matrix, so the same decision, on every rank.  Collective (one allgather).
+void Comm::classify_topology(const void* records) {
+  const PeerInfo* all = static_cast<const PeerInfo*>(records);
+  const int n = nranks_;
+  struct Row {
+    int32_t link[kMaxRanks], hops[kMaxRanks];
+  } mine;
+  for (int p = 0; p < kMaxRanks; ++p) {
+    mine.link[p] = kPeerSameGpu;
+    mine.hops[p] = 0;
+  }
+  for (int p = 0; p < n; ++p) {
+    if (p == rank_ || all[p].pci == all[rank_].pci) continue;
+    const int pd = local_device_with_pci(all[p].pci);
+    uint32_t lt = 0, hc = 0;
+    if (pd < 0 || hipExtGetLinkTypeAndHopCount(device_, pd, &lt, &hc) != hipSuccess) {
+      (void)hipGetLastError();
+      mine.link[p] = kPeerUnknown;
+      mine.hops[p] = -1;
+    } else {
+      mine.link[p] = (int32_t)lt;
+      mine.hops[p] = (int32_t)hc;
+    }
+  }
+  std::vector<Row> rows((size_t)n);
+  boot_.allgather(&mine, rows.data(), sizeof mine);
+  std::vector<int> link((size_t)n * n), hops((size_t)n * n);
+  for (int q = 0; q < n; ++q)
+    for (int p = 0; p < n; ++p) {
+      link[(size_t)q * n + p] = rows[(size_t)q].link[p];
+      hops[(size_t)q * n + p] = rows[(size_t)q].hops[p];
+    }
+  for (int p = 0; p < kMaxRanks; ++p) {
+    peer_link_[p] = p < n ? mine.link[p] : kPeerSameGpu;
+    peer_hops_[p] = p < n ? mine.hops[p] : 0;
+  }
+  const int bad = topology_blocks_read(n, link.data(), hops.data());
+  topo_read_ = bad == 0;
+  char why[160];
+  if (bad == 0) {
+    snprintf(why, sizeof why, "read: every pair of ranks shares a GPU or is one xGMI hop apart");
+  } else {
+    const int q = (bad - 1) / n, p = (bad - 1) % n, l = link[(size_t)bad - 1];
+    const char* name = l == kPeerUnknown ? "an unknown link (its GPU is not visible to that process)"
+                       : l == kLinkPcie  ? "PCIe"
+                       : l == kLinkXgmi  ? "xGMI"
+                                         : "a non-xGMI link";
+    snprintf(why, sizeof why, "ring: rank %d reaches rank %d over %s, %d hop(s)", q, p, name, hops[(size_t)bad - 1]);
+    if (rank_ == 0 && auto_)
+      fprintf(stderr, "[Mini-NCCL] auto: the read schedule is off for this communicator (%s); calls run the ring "
+              "(MINI_NCCL_ALGO=read forces it)\n", why);
+  }
+  topo_why_ = why;
+}
+
 Comm::~Comm() {
   hipSetDevice(device_);
   // the last call may still run (stream-ordered mode): its kernel writes into the peers' scratch
@@ -293,9 +353,13 @@ Comm::~Comm() {
     }
   }
   // this communicator's kernels are done (waited above): its imports of peers no other live
-  // communicator of this process talks to are closed, and the exports too if it was the last one
-  // (a failed communicator's peers may still read this process's memory: then keep everything)
-  if (registered_ && sticky_ == ncclSuccess) ipc::comm_closed(owners_);
+  // communicator of this process talks to are closed, and the exports too if it was the last one.
+  // Also after a failure (skipping this pinned every export of the process for good):
+  // a peer whose kernel still runs reads and writes this process's buffers through ITS imports,
+  // which hold their own reference on the memory -- closing this process's export descriptors or
+  // its own (idle) imports cannot pull memory from under it.  What a failed peer may still write
+  // into -- this communicator's scratch and mailbox -- stays out of the pool (release()).
+  if (registered_) ipc::comm_closed(owners_);
   registered_ = false;
   release();
 }
@@ -319,6 +383,7 @@ void Comm::release() {
   scratch_ = nullptr;
   mbox_ = nullptr;
   pair_seq_ = nullptr;
+  claim_ = nullptr;
   h_ctl_ = nullptr;
   (void)hipGetLastError();
 }
@@ -487,6 +552,7 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.sys_fence = cfg_.sys_fence;
   p.read_push = cfg_.read_push;
   p.tail_bytes = tail_bytes;
+  p.claim = claim_;
   const int nt = cfg_.threads, wg = A / geo_.waves;
   hipError_t e = algo == 2   ? launch_read(dtype, op, vec, wg, nt, p, stream)
                  : algo == 3 ? launch_oneshot(dtype, op, vec, wg, nt, p, stream)
@@ -550,7 +616,10 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     // all ranks decide alike.
     const bool oneshot = algo_ == 3 && oneshot_fits(chunk_bytes, n, wave_channels(), wave_slice(), true);
     const bool small = auto_ && oneshot_fits(chunk_bytes, n, wave_channels(), wave_slice(), false);
-    const bool read_sched = !oneshot && (algo_ == 2 || algo_ == 3) && pbuf_.available();
+    // (auto, and a forced one-shot's larger calls, only where the topology allows the read
+    // schedule: classify_topology; MINI_NCCL_ALGO=read forces it anywhere)
+    const bool read_sched =
+        !oneshot && ((algo_ == 2 && (!auto_ || topo_read_)) || (algo_ == 3 && topo_read_)) && pbuf_.available();
     if (read_sched) pbuf_.reap(send, recv);
     const Reach rs = read_sched && pbuf_.known(send) ? (local_s = true, Reach::kDevice) : reach(send, &ksend, &local_s);
     const Reach rr = read_sched && pbuf_.known(recv) ? (local_r = true, Reach::kDevice)

@@ -44,6 +44,12 @@ class Comm {
   const PeerBuffers& peer_buffers() const { return pbuf_; }
   // rank processes / communicators whose GPU is this rank's GPU (this rank included)
   int ranks_on_device() const { return ranks_on_device_; }
+  // auto's topology rule (schedule.h topology_blocks_read), the same on every rank: whether the
+  // default runs the read schedule, why, and how this rank's GPU reaches each peer's
+  bool topology_allows_read() const { return topo_read_; }
+  const std::string& topology_reason() const { return topo_why_; }
+  int peer_link(int q) const { return peer_link_[q]; }
+  int peer_hops(int q) const { return peer_hops_[q]; }
   ncclResult_t async_error();
   // Collective: every rank writes `bytes` into the next rank's scratch (all_peers = 0) or into
   // every peer's scratch at once (1), `iters` times; *gbps = bytes per second per link
@@ -60,6 +66,7 @@ class Comm {
   void setup_device_resources();
   void release();
   void exchange_and_map();
+  void classify_topology(const void* records);  // records: every rank's init record (comm.cpp)
   ncclResult_t wait_for(hipStream_t stream, uint32_t seq);
   enum class Reach { kDevice, kMapped, kStaged };
   Reach reach(const void* p, const void** kernel_ptr, bool* local) const;
@@ -83,6 +90,9 @@ class Comm {
   bool auto_ = true;             // the default: as algo_ = 2, with the ring's small calls one-shot
   int last_algo_ = -1;
   int ranks_on_device_ = 1;
+  bool topo_read_ = true;        // auto may run the read schedule (every pair: same GPU or 1 xGMI hop)
+  std::string topo_why_ = "read: one rank";
+  int peer_link_[kMaxRanks] = {}, peer_hops_[kMaxRanks] = {};
   uint32_t call_seq_ = 0;        // kernel launches of this communicator (the kernel's start word)
   Bootstrap boot_;
 
@@ -91,6 +101,7 @@ class Comm {
   uint64_t* mbox_ = nullptr;     // uncached device memory: READY / CREDIT / ABORT words
   size_t mbox_bytes_ = 0;
   uint64_t* pair_seq_ = nullptr; // [2][n][C]: per (peer, channel) tx / rx message counters (device)
+  uint32_t* claim_ = nullptr;    // after them: the kernels' first-give-up word (kernels.h)
   uint32_t* h_ctl_ = nullptr;    // host-mapped: [0] status, [1] abort request, [2] last started call
   uint32_t* d_ctl_ = nullptr;    // device view of h_ctl_
 

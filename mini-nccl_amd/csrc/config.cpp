@@ -22,9 +22,37 @@ long long env_int(const char* name, long long dflt) {
   return x;
 }
 
+// Knobs of earlier versions that are gone: set, they would otherwise be ignored silently (a 3.x
+// deployment's STAGE_HOST=1 staged pinned buffers; now the kernel always maps them).  Warned once
+// per process, naming what replaced each.
+void warn_removed_knobs() {
+  static bool warned = false;
+  if (warned) return;
+  warned = true;
+  static const struct {
+    const char* name;
+    const char* now;
+  } removed[] = {
+      {"MINI_NCCL_PULL", "removed in 4.0 with the direct schedule; MINI_NCCL_READ_PUSH=0 is the load form of read"},
+      {"MINI_NCCL_DIRECT_OVERLAP", "removed in 4.0 with the direct schedule"},
+      {"MINI_NCCL_CALIBRATE", "removed in 4.0: auto decides per call (and, since 5.0, from the topology)"},
+      {"MINI_NCCL_CALIBRATE_BYTES", "removed in 4.0 with MINI_NCCL_CALIBRATE"},
+      {"MINI_NCCL_PIPE_DEPTH", "removed in 4.0: one slice per pipeline per iteration, sized by the call"},
+      {"MINI_NCCL_MIN_SLICE", "removed in 4.0: the adaptive payload's floor is 1 KiB"},
+      {"MINI_NCCL_STAGE_HOST", "removed in 4.0: pinned host buffers are always mapped into the kernel, "
+                               "pageable ones staged"},
+      {"MINI_NCCL_TUNE", "removed in 3.0.1: no init-time calibration"},
+  };
+  for (const auto& k : removed) {
+    const char* v = std::getenv(k.name);
+    if (v && *v) fprintf(stderr, "[Mini-NCCL] warning: %s=%s is ignored (%s)\n", k.name, v, k.now);
+  }
+}
+
 }  // namespace
 
 Config Config::from_env() {
+  warn_removed_knobs();
   Config c;
   long long slice = env_int("MINI_NCCL_SLICE_SIZE", 128 * 1024);
   if (slice <= 0) slice = 1024;  // Config.h:50 maps 0 -> 1024

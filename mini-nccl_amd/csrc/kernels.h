@@ -38,6 +38,8 @@ struct CollParams {
   const char* peer_recv[16];  // read schedule: every rank's recv buffer, mapped here
   uint64_t tail_bytes;        // bytes past n * chunk_bytes that the kernel copies send -> recv
                               // (the reference leaves them as its copy made them, api.cpp:173-175)
+  uint32_t* claim;            // device word, 0 until the communicator's first give-up claims it:
+                              // only that lane writes the status and its diagnostic
 };
 
 constexpr int kMaxRanks = 16;

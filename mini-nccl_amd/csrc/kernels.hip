@@ -177,27 +177,39 @@ struct Ctl {
   const uint32_t* host_abort;
   const u64* my_abort;
   uint64_t timeout_ticks;
-  const u64* mbox;  // this rank's mailbox base (for the timeout diagnostic)
+  const u64* mbox;   // this rank's mailbox base (for the timeout diagnostic)
+  uint32_t* claim;   // device word: the first give-up of the communicator takes it (claim_first)
 };
 
+// The first give-up -- a timeout, a peer's ABORT, the host's abort -- of any lane of any wave
+// claims the status with one agent-scope compare-and-swap on a device word (the host-mapped
+// status page itself takes no atomics: no PCIe atomics needed), so the cause and the diagnostic
+// the host reports come from ONE lane: lanes of wave_wait_peers that give up in the same round,
+// or a timeout racing a peer's ABORT, can no longer mix their words or overwrite the first cause
+// (ADVICE r4).  The winner writes its words, then the status; the others just give up.
+__device__ __forceinline__ bool claim_first(const Ctl& c) {
+  uint32_t expected = 0;
+  return __hip_atomic_compare_exchange_strong(c.claim, &expected, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // a timed-out wait: which mailbox word, the target and the last value seen (host-mapped words
-// 4..9 of the control page; plain system-scope stores, no PCIe atomics; only the first wave to
-// time out -- the others see a non-zero status -- normally writes them)
+// 4..6 of the control page, plain system-scope stores), then the status
 __device__ __forceinline__ void record_timeout(const Ctl& c, const u64* flag, u64 target, u64 seen) {
-  if (ld_sys32(c.status) != 0) return;
+  if (!claim_first(c)) return;
   u64* diag = reinterpret_cast<u64*>(c.status + 4);
   __hip_atomic_store(diag + 0, (u64)(flag - c.mbox), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(diag + 1, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(diag + 2, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  st_sys32(c.status, kStatusTimeout);
 }
 
-// a peer's ABORT word seen: the first cause stays in the status word (a peer's abort that
-// echoes this rank's own timeout must not hide it); the word names the peer and its cause
+// a peer's ABORT word seen: recorded only as the first cause (a peer's abort that echoes this
+// rank's own timeout must not hide it); the word names the peer and its cause
 __device__ __forceinline__ void note_remote_abort(const Ctl& c, u64 a) {
-  if (ld_sys32(c.status) == 0) {
-    __hip_atomic_store(reinterpret_cast<u64*>(c.status + 4) + 3, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    st_sys32(c.status, kStatusRemoteAbort);
-  }
+  if (!claim_first(c)) return;
+  __hip_atomic_store(reinterpret_cast<u64*>(c.status + 4) + 3, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  st_sys32(c.status, kStatusRemoteAbort);
 }
 
 // lane-0 spin until *flag >= target; false on timeout / abort (status already set).  The
@@ -217,13 +229,12 @@ __device__ __noinline__ bool wait_ge_spin(const u64* flag, u64 target, const Ctl
         return false;
       }
       if (ld_sys32(c.host_abort) != 0) {
-        if (ld_sys32(c.status) == 0) st_sys32(c.status, kStatusHostAbort);
+        if (claim_first(c)) st_sys32(c.status, kStatusHostAbort);
         return false;
       }
       if (ld_sys32(c.status) != 0) return false;  // a sibling workgroup gave up
       if (__builtin_amdgcn_s_memrealtime() - t0 > c.timeout_ticks) {
         record_timeout(c, flag, target, ld_sys(flag));
-        st_sys32(c.status, kStatusTimeout);
         return false;
       }
     }
@@ -433,7 +444,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) ring_kernel(Col
   const int n = p.n, r = p.rank, K = p.nslots;
   copy_tail(p, w, lane);
   const int prev = mod_n(r - 1, n), next = mod_n(r + 1, n);
-  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox};
+  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox, p.claim};
   // per-pair message counters: the FIFO to `next` and the FIFO from `prev` on this channel
   u64* tx_ctr = p.tx_seq + (u64)next * C + w;
   u64* rx_ctr = p.rx_seq + (u64)prev * C + w;
@@ -783,7 +794,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
   __shared__ u64 s_tx[kMaxWaves][kMaxRanks], s_rx[kMaxWaves][kMaxRanks];
   u64* tx = s_tx[wv];
   u64* rx = s_rx[wv];
-  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox};
+  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox, p.claim};
   const uint32_t iters = p.iters;
   const u64 mpc = read_msgs_per_call(iters);
   if (lane < n) {
@@ -891,7 +902,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) oneshot_kernel(
   __shared__ u64 s_tx[kMaxWaves][kMaxRanks], s_rx[kMaxWaves][kMaxRanks];
   u64* tx = s_tx[wv];
   u64* rx = s_rx[wv];
-  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox};
+  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox, p.claim};
   if (lane < n) {
     tx[lane] = p.tx_seq[(u64)lane * C + w];
     rx[lane] = p.rx_seq[(u64)lane * C + w];

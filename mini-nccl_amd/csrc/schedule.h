@@ -241,6 +241,30 @@ MNCCL_HD uint64_t msg_slot_off(int C, int slots, uint64_t slot_bytes, int src, i
   return scratch_slot_off(C, slots, slot_bytes, region_index(dst, src), w, seq);
 }
 
+// Topology rule of the default schedule (MINI_NCCL_ALGO=auto).  The read schedule loads from and
+// pushes into every peer's memory directly, so it is only the fast path when every pair of GPUs
+// is one xGMI hop apart -- an MI355X node's full mesh; over PCIe (or a multi-hop route) every
+// byte would cross the host fabric and the ring, which moves 2(n-1)/n of the buffer through one
+// neighbour link, is the safer choice.  Ranks sharing a GPU (the reference's perf_test topology)
+// reach each other through that GPU's own memory: allowed.  A peer whose GPU this process cannot
+// see cannot be classified: not allowed (the runtime could not tell us the link).  The reference
+// decides per peer whether its same-host IPC path applies (RDMATransport.h:109-111,583-590);
+// here every rank applies this to its own row and the communicator takes the AND over ranks
+// (Comm::exchange_and_map), so every rank decides alike.  link[q * n + p] / hops[q * n + p]: how
+// rank q's GPU reaches rank p's (kPeerSameGpu, kPeerUnknown, or the HSA link type: 2 PCIe, 4 xGMI).
+enum : int { kPeerSameGpu = -1, kPeerUnknown = -2, kLinkPcie = 2, kLinkXgmi = 4 };
+// 0: the read schedule may be the default; otherwise 1 + the first offending pair's index q * n + p
+MNCCL_HD int topology_blocks_read(int n, const int* link, const int* hops) {
+  for (int q = 0; q < n; ++q)
+    for (int p = 0; p < n; ++p) {
+      if (p == q) continue;
+      const int l = link[q * n + p];
+      if (l == kPeerSameGpu) continue;
+      if (l != kLinkXgmi || hops[q * n + p] != 1) return 1 + q * n + p;
+    }
+  return 0;
+}
+
 // Kernel status bits (host-mapped status word)
 enum : uint32_t { kStatusTimeout = 1u, kStatusHostAbort = 2u, kStatusRemoteAbort = 4u };
 

@@ -275,6 +275,9 @@ uint64_t mnccl_read_slice(uint64_t chunk_bytes, int channels, uint64_t slice, ui
 
 int mnccl_call_pipelines(uint64_t nslices, int channels, int waves) { return call_pipelines(nslices, channels, waves); }
 
+// schedule.h topology_blocks_read over an n x n matrix (rank q's row: how q's GPU reaches p's)
+int mnccl_topology_blocks_read(int n, const int* link, const int* hops) { return topology_blocks_read(n, link, hops); }
+
 // Runs `calls` consecutive all-reduces (send -> recv, fp32; send == recv for in place) on n
 // simulated ranks with the GPU kernels' protocol; call i uses schedule (algo >> 2i) & 3 (0 ring,
 // 1 one-shot, 2 read in its push form, 3 read in its load form; schedules can alternate on one

@@ -56,6 +56,9 @@ class CommInfo(ctypes.Structure):
         ("read_rounds", ctypes.c_ulonglong), ("closed_freed", ctypes.c_ulonglong), ("live_exports", ctypes.c_size_t),
         # since mncclVersion 400
         ("cap_refusals", ctypes.c_ulonglong), ("liveness_queries", ctypes.c_ulonglong), ("read_push", ctypes.c_int),
+        # since mncclVersion 500
+        ("auto_read", ctypes.c_int), ("peer_link", ctypes.c_int * 16), ("peer_hops", ctypes.c_int * 16),
+        ("auto_reason", ctypes.c_char * 160),
     ]
 
 
@@ -141,6 +144,10 @@ class Comm:
         d = {f: getattr(i, f) for f, _ in CommInfo._fields_}
         d["tune_ms"] = list(d["tune_ms"])
         d["calib_ms"] = list(d["calib_ms"])
+        n = d["nranks"]
+        d["peer_link"] = list(d["peer_link"])[:n]
+        d["peer_hops"] = list(d["peer_hops"])[:n]
+        d["auto_reason"] = d["auto_reason"].decode(errors="replace")
         return d
 
     PROBE_FORMS = {"sys": 0, "nt": 1, "plain": 2}

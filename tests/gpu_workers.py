@@ -1,10 +1,14 @@
 """Rank processes for the multi-process GPU tests (spawned; one process = one rank).
 
-The reference tests several ranks sharing GPU 0 (tests/perf_test.cpp:46); the 1-GPU
-test box does the same: every rank opens the others' scratch/mailbox through HIP IPC
-on the same device, so the whole cross-process protocol (bootstrap, IPC mapping,
-flags, credits, sequence continuation, aborts) runs for real.  The oracle each rank
-compares against is computed in-process from the same seeded inputs.
+Placement (rank_device): rank r runs on GPU r % ndev of the box -- one rank per GPU on a
+multi-GPU box, as the node runs (so the suite, unedited, is a cross-device parity run over
+xGMI there) -- and every rank on GPU 0 on a 1-GPU box or under MNCCL_TEST_COLOCATE=1 (the
+reference's perf_test topology, tests/perf_test.cpp:46).  Co-located, every rank opens the
+others' scratch / mailbox / buffers through IPC on the same device, so the whole cross-process
+protocol (bootstrap, IPC mapping, flags, credits, sequence continuation, aborts) still runs
+for real.  Every rank reports the device and the ranks_on_device its communicator saw, and the
+tests check them against the placement they asked for.  The oracle each rank compares
+against is computed in-process from the same seeded inputs.
 """
 import os
 import sys
@@ -18,6 +22,35 @@ ROOT = os.path.dirname(HERE)
 for p in (HERE, os.path.join(ROOT, "mini-nccl_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)
+
+
+def colocated(env=None):
+    """MNCCL_TEST_COLOCATE=1: every rank on GPU 0 whatever the box (today's 1-GPU layout)."""
+    v = (env if env is not None else os.environ).get("MNCCL_TEST_COLOCATE", "0")
+    return v not in ("", "0")
+
+
+def rank_device(rank, ndev, colocate=None):
+    """The GPU rank `rank` runs on, given `ndev` visible GPUs: rank % ndev, or 0 when co-located."""
+    if colocate is None:
+        colocate = colocated()
+    return 0 if colocate or ndev < 2 else rank % ndev
+
+
+def ranks_sharing_device(rank, n, ndev, colocate=None):
+    """Ranks of an n-rank communicator on `rank`'s GPU (itself included): the communicator's
+    mncclCommInfo_t.ranks_on_device under this placement."""
+    d = rank_device(rank, ndev, colocate)
+    return sum(1 for q in range(n) if rank_device(q, ndev, colocate) == d)
+
+
+def use_rank_device(rank):
+    """In a rank process: select rank_device(rank) (TEST_DEVICE=<d> overrides) and return it."""
+    import hip_rt
+    d = os.environ.get("TEST_DEVICE")
+    d = int(d) if d not in (None, "") else rank_device(rank, hip_rt.device_count())
+    hip_rt.set_device(d)
+    return d
 
 
 def _bits(a):
@@ -57,7 +90,7 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
         import hip_rt
         import mini_nccl as M
         import oracle_api as O
-        hip_rt.set_device(int(env.get("TEST_DEVICE", "0")))
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         stream = hip_rt.Stream()
         results = []
@@ -153,7 +186,7 @@ def many_buffers_rank(rank, n, port, env, pairs, out_q):
         import hip_rt
         import mini_nccl as M
         import oracle_api as O
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         comm.set_algo(2)
         st = hip_rt.Stream()
@@ -200,7 +233,7 @@ def release_rank(rank, n, port, env, nbytes, out_q, barrier=None):
         os.environ["MINI_NCCL_PORT"] = str(port)
         import hip_rt
         import mini_nccl as M
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         comm.set_algo(2)
         count = nbytes // 4
@@ -238,7 +271,7 @@ def two_comms_rank(rank, n, ports, env, rounds, out_q):
         import hip_rt
         import mini_nccl as M
         import oracle_api as O
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comms = []
         for p in ports:
             os.environ["MINI_NCCL_PORT"] = str(p)
@@ -315,7 +348,7 @@ def fullsize_rank(rank, n, port, env, dtype, count, algos, out_q, barrier=None):
         import hip_rt
         import mini_nccl as M
         import oracle_api as O
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         x = fullsize_input(rank, count, dtype)
         code, npd = O.DTYPES[dtype]
         comm = M.Comm(n, rank, "127.0.0.1")
@@ -358,7 +391,7 @@ def graph_rank(rank, n, port, env, replays, out_q):
         import hip_rt
         import mini_nccl as M
         import oracle_api as O
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         st = hip_rt.Stream()
         count = (1 << 18) + 1
@@ -404,7 +437,7 @@ def streams_rank(rank, n, port, env, calls, out_q):
         import hip_rt
         import mini_nccl as M
         import oracle_api as O
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         sts = [hip_rt.Stream(), hip_rt.Stream()]
         count = (1 << 20) + 3
@@ -443,7 +476,7 @@ def probe_rank(rank, n, port, env, out_q):
         import hip_rt
         import mini_nccl as M
         import oracle_api as O
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         res = {"next": comm.link_probe(False, 8 << 20, 3), "mesh": comm.link_probe(True, 8 << 20, 3)}
         # the comparison forms (push nt / default policy, pull) on the same links
@@ -475,7 +508,7 @@ def init_rank(rank, n, port, env, out_q):
         import ctypes
         import hip_rt
         import mini_nccl as M
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         h = ctypes.c_void_p()
         rc = M.load().ncclCommInitRank(ctypes.byref(h), n, rank, b"127.0.0.1")
         if rc == 0:
@@ -495,7 +528,7 @@ def mismatch_rank(rank, n, port, env, out_q):
         import hip_rt
         import mini_nccl as M
         import oracle_api as O
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         st = hip_rt.Stream()
         count = 40000
@@ -524,7 +557,7 @@ def info_rank(rank, n, port, env, out_q):
         os.environ["MINI_NCCL_PORT"] = str(port)
         import hip_rt
         import mini_nccl as M
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         info = comm.info()
         out_q.put((rank, {"info": info, "destroy": comm.destroy()}))
@@ -540,7 +573,7 @@ def huge_rank(rank, n, port, env, count, out_q):
         os.environ["MINI_NCCL_PORT"] = str(port)
         import hip_rt
         import mini_nccl as M
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         buf = hip_rt.DeviceBuffer(count * 2)
         chunk = 1 << 26
@@ -574,7 +607,7 @@ def destroy_inflight_rank(rank, n, port, env, out_q):
         os.environ["MINI_NCCL_PORT"] = str(port)
         import hip_rt
         import mini_nccl as M
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         stream = hip_rt.Stream()
         count = (64 << 20) // 4
@@ -600,7 +633,7 @@ def stall_rank(rank, n, port, env, call_allreduce, out_q):
         os.environ["MINI_NCCL_PORT"] = str(port)
         import hip_rt
         import mini_nccl as M
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         buf = hip_rt.DeviceBuffer(1 << 20)
         res = {}
@@ -638,7 +671,7 @@ def delayed_start_rank(rank, n, port, env, delay_s, out_q):
         import hip_rt
         import mini_nccl as M
         import oracle_api as O
-        hip_rt.set_device(0)
+        use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         st = hip_rt.Stream()
         count = (1 << 20) + 3
@@ -716,6 +749,72 @@ def local_reduce_in_place_large():
     finally:
         da.free()
         db.free()
+
+
+def testkern():
+    """tests/lib/libmnccl_testkern.so: plain-load consumer kernels (test infrastructure)."""
+    import ctypes
+    L = ctypes.CDLL(os.path.join(HERE, "lib", "libmnccl_testkern.so"))
+    vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+    L.mnccl_test_touch.argtypes = [vp, u64, vp, vp]
+    L.mnccl_test_copy.argtypes = [vp, vp, u64, vp]
+    return L
+
+
+def cached_consumer_rank(rank, n, port, env, count, calls, out_q, barrier=None):
+    """VERDICT r4 #1, the push form's cross-device visibility in the shape the node gives it: recv
+    is first read by an ordinary kernel (plain loads: its lines sit in this GPU's L2), then the
+    read schedule's call -- the peers push their result chunks into this recv (from other GPUs over
+    xGMI when the placement spreads the ranks, from other XCDs' L2s when they share a GPU) -- and an
+    ordinary consumer kernel copies recv with plain loads right behind the call on the same stream
+    (MINI_NCCL_BLOCKING=0: no host wait in between).  Seeded uniform[-1, 1) inputs, new every call
+    (order-sensitive: a wrong association, a stale line or a torn push each change bits), compared
+    bit for bit with the oracle's ring fold."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import ctypes
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        use_rank_device(rank)
+        K = testkern()
+        comm = M.Comm(n, rank, "127.0.0.1")
+        comm.set_algo(int(env.get("TEST_ALGO", "2")))
+        st = hip_rt.Stream()
+        nb = count * 4
+        send, recv, seen = hip_rt.DeviceBuffer(nb), hip_rt.DeviceBuffer(nb), hip_rt.DeviceBuffer(nb)
+        word = hip_rt.DeviceBuffer(256)
+        bad, rcs, algos = [], [], []
+        for c in range(calls):
+            inplace = c % 3 == 2
+            dst = send if inplace else recv
+            xs = O.random_inputs(n, count, "f32", seed=4000 + 17 * c)
+            exp = O.allreduce(xs, "f32", "sum", inplace=inplace)[rank]
+            send.upload(xs[rank])
+            hip_rt.sync()
+            if barrier is not None:
+                barrier.wait(120)
+            # the previous call's result (or the fresh input, in place) into this GPU's L2 ...
+            hip_rt.check(K.mnccl_test_touch(ctypes.c_void_p(dst.ptr), nb, ctypes.c_void_p(word.ptr),
+                                            ctypes.c_void_p(st.handle)), "touch")
+            rc = comm.all_reduce(send.ptr, dst.ptr, count, M.ncclFloat, M.ncclSum, st.handle)
+            # ... and read by an ordinary kernel right after the call
+            hip_rt.check(K.mnccl_test_copy(ctypes.c_void_p(seen.ptr), ctypes.c_void_p(dst.ptr), nb,
+                                           ctypes.c_void_p(st.handle)), "copy")
+            st.sync()
+            rcs.append(rc)
+            algos.append(comm.info()["last_algo"])
+            got = seen.download(np.float32, count)
+            bad.append(compare(got, exp, "f32", True)[0])
+        info = comm.info()
+        for b in (send, recv, seen, word):
+            b.free()
+        st.destroy()
+        out_q.put((rank, {"rcs": rcs, "bad": bad, "algos": algos, "info": info, "async": comm.async_error(),
+                          "destroy": comm.destroy()}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
 
 
 def device_count_probe(out_q):

@@ -24,6 +24,7 @@ def load():
         L.mnccl_read_slice.argtypes = [u64, i, u64, u64, i]
         L.mnccl_read_slice.restype = u64
         L.mnccl_call_pipelines.argtypes = [u64, i, i]
+        L.mnccl_topology_blocks_read.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(i)]
         L.mnccl_oneshot_slice.argtypes = [u64, i, i, u64]
         L.mnccl_oneshot_slice.restype = u64
         L.mnccl_oneshot_fits.argtypes = [u64, i, i, u64, i]
@@ -107,3 +108,17 @@ def board_selftest(rank, nranks, port, scenario, calls, timeout_s=2.0):
     dec = (ctypes.c_int * calls)()
     rc = load().mnccl_board_selftest(rank, nranks, b"127.0.0.1", port, scenario, calls, timeout_s, dec)
     return rc, list(dec)
+
+
+# schedule.h link kinds (how rank q's GPU reaches rank p's)
+SAME_GPU, UNKNOWN, PCIE, XGMI = -1, -2, 2, 4
+
+
+def topology_blocks_read(link, hops):
+    """csrc/schedule.h topology_blocks_read on an n x n link / hop matrix (row q: rank q's view):
+    None when auto may run the read schedule, else the first offending pair (q, p)."""
+    n = len(link)
+    flat_l = (ctypes.c_int * (n * n))(*[link[q][p] for q in range(n) for p in range(n)])
+    flat_h = (ctypes.c_int * (n * n))(*[hops[q][p] for q in range(n) for p in range(n)])
+    bad = load().mnccl_topology_blocks_read(n, flat_l, flat_h)
+    return None if bad == 0 else divmod(bad - 1, n)

@@ -93,7 +93,7 @@ def test_argument_checks_before_device_work(nccl_lib):
     assert L.mncclLocalReduce(fake, fake, fake, 4, M.ncclFloat, M.ncclAvg, None) == M.ncclInternalError
     assert L.mncclLocalReduce(None, fake, fake, 4, M.ncclFloat, M.ncclSum, None) == M.ncclInvalidArgument
     assert L.mncclCommSetAlgo(None, 0) == M.ncclInvalidArgument
-    assert L.mncclVersion() == 401
+    assert L.mncclVersion() == 500
 
 
 def test_info_struct_layout(nccl_lib):
@@ -209,3 +209,24 @@ def test_pipeline_geometry(sim_lib):
     assert g["workgroups"] == 1 and g["slot_bytes"] % 1024 == 0 and g["scratch_bytes"] <= 512 * MiB
     g = S.pipeline_geometry(8, cap=16 * MiB, slice_bytes=1 << 20)
     assert g["workgroups"] == 1 and g["scratch_bytes"] <= 16 * MiB
+
+
+def test_removed_knobs_are_warned_once(sim_lib):
+    # a knob removed in 4.0 that is still set (a 3.x deployment's MINI_NCCL_STAGE_HOST=1
+    # used to stage pinned buffers) is named on stderr once per process, with what replaced it
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import sim_api as S\n"
+            "for _ in range(3): S.config_describe()\n") % os.path.dirname(os.path.abspath(__file__))
+    env = {k: v for k, v in os.environ.items() if not k.startswith("MINI_NCCL_")}
+    env.update(MINI_NCCL_STAGE_HOST="1", MINI_NCCL_PIPE_DEPTH="4")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stderr.splitlines() if "is ignored" in ln]
+    assert len(lines) == 2, r.stderr
+    assert any("MINI_NCCL_STAGE_HOST=1" in ln and "always mapped" in ln for ln in lines)
+    assert any("MINI_NCCL_PIPE_DEPTH=4" in ln for ln in lines)
+    env.pop("MINI_NCCL_STAGE_HOST")
+    env.pop("MINI_NCCL_PIPE_DEPTH")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
+    assert "is ignored" not in r.stderr

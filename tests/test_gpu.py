@@ -2,8 +2,11 @@
 
 * mncclLocalReduce (the scatter-reduce element-wise kernel alone) vs oracle_reduce,
   every dtype x op, vector and scalar (misaligned / odd-size) paths, bit-exact;
-* ncclAllReduce with 2-10 rank processes sharing GPU 0 (as the reference's perf_test
-  does, tests/perf_test.cpp:46), the ring and the read schedule (push form, and its load
+* ncclAllReduce with 2-10 rank processes, rank r on GPU r % ndev (one rank per GPU on a
+  multi-GPU box: a cross-device run over xGMI) or all on GPU 0 on a 1-GPU box / under
+  MNCCL_TEST_COLOCATE=1 (as the reference's perf_test does, tests/perf_test.cpp:46), every
+  rank's device and co-located rank count checked against that placement; the ring and the
+  read schedule (push form, and its load
   form MINI_NCCL_READ_PUSH=0 where the protocol differs), in/out of place, odd counts
   (tail), repeated calls, slices smaller than a chunk, bit-exact vs the oracle (NaN
   payloads of +/* excepted: NaN-ness must match);
@@ -35,7 +38,25 @@ def dev(nccl_lib, oracle_lib):
     out = GW.run_ranks(GW.device_count_probe, 1, lambda r: (), 120)
     if not out or out[0]["count"] < 1:
         pytest.fail("no HIP device visible: the -m gpu suite must run on the MI355X box")
-    return True
+    # placement (gpu_workers.rank_device): rank r on GPU r % ndev, every rank on GPU 0 on a 1-GPU
+    # box or under MNCCL_TEST_COLOCATE=1
+    NDEV[0] = out[0]["count"]
+    print(f"\n[placement] {NDEV[0]} GPU(s) visible, co-located={GW.colocated()}: rank r on GPU "
+          f"{'0' if GW.colocated() or NDEV[0] < 2 else 'r % ' + str(NDEV[0])}")
+    return NDEV[0]
+
+
+NDEV = [1]  # GPUs the rank processes see (set by the `dev` fixture)
+
+
+def _check_placement(r, n, info, env=None):
+    """rank r's communicator ran where the placement put it, with the right co-located ranks"""
+    colo = GW.colocated(dict(os.environ, **(env or {})))
+    want = GW.rank_device(r, NDEV[0], colo)
+    if "TEST_DEVICE" in (env or {}):
+        return
+    assert info["device"] == want, f"rank {r}: device {info['device']}, placement asked for {want}"
+    assert info["ranks_on_device"] == GW.ranks_sharing_device(r, n, NDEV[0], colo), (r, n, NDEV[0], info)
 
 
 class TestLocalReduce:
@@ -70,6 +91,7 @@ def _run_allreduce(n, cases, env=None, timeout=300, barrier=True):
     for r in range(n):
         assert "error" not in out[r], f"rank {r}:\n{out[r]['error']}"
         assert out[r]["destroy"] == 0
+        _check_placement(r, n, out[r]["info"], env)
         for res in out[r]["results"]:
             c = res["case"]
             assert res["rc"] == 0, f"rank {r} case {c}: ncclResult {res['rc']}"
@@ -155,7 +177,8 @@ def test_auto_schedule_no_init_allreduce(dev):
         # here (the one-shot for small ones)
         assert i["tune_ms"] == [0.0, 0.0] and i["algo"] == -1 and i["scratch_algo"] == 0, i
         assert i["read_push"] == 1 and i["calib_choice"] == -1 and i["calib_ms"] == [0.0, 0.0], i
-        assert i["ranks_on_device"] == 3 and i["last_algo"] == -1, i
+        _check_placement(r, 3, i)
+        assert i["last_algo"] == -1, i
         assert i["channels"] == 256 and i["pipelines"] == 256 and i["slot_bytes"] == 128 << 10
         assert i["scratch_bytes"] == 2 * 256 * 2 * (128 << 10)  # (n-1) peer regions
     port = GW.free_port()
@@ -272,6 +295,28 @@ def test_oneshot_10_ranks(dev):
              _case(count=12345, algo=3, seed=46, calls=3, vary=True)]
     env = {"MINI_NCCL_CHANNELS": "64", "GPU_MAX_HW_QUEUES": "1"}
     _run_allreduce(10, cases, env, timeout=600)
+
+
+@pytest.mark.parametrize("n,algo,env", [(2, 2, {}), (3, 2, {}), (8, 2, {"GPU_MAX_HW_QUEUES": "2"}),
+                                        (3, 2, LOAD_FORM), (3, 0, {})],
+                         ids=["read_n2", "read_n3", "read_n8", "read_load_n3", "ring_n3"])
+def test_read_push_visible_to_cached_consumers(dev, n, algo, env):
+    # recv's lines pre-warmed into its owner's L2 by an ordinary kernel, then a call
+    # whose peers push into that recv (other GPUs over xGMI when the placement spreads the ranks,
+    # other XCDs' L2s when they share one), then an ordinary plain-load consumer right behind the
+    # call on the same stream: seeded uniform data, every call bit-exact vs the oracle's ring fold
+    port = GW.free_port()
+    count = (1 << 20) + 2 * n + 1
+    e = {"MINI_NCCL_TIMEOUT_MS": "30000", "MINI_NCCL_BLOCKING": "0", "TEST_ALGO": str(algo), **env}
+    out = GW.run_ranks(GW.cached_consumer_rank, n, lambda r: (r, n, port, e, count, 6), 600, barrier=True)
+    assert sorted(out) == list(range(n)), out
+    for r in range(n):
+        o = out[r]
+        assert "error" not in o, o["error"]
+        _check_placement(r, n, o["info"])
+        assert o["rcs"] == [0] * 6 and o["async"] == 0 and o["destroy"] == 0, o
+        assert o["algos"] == [algo] * 6, o["algos"]
+        assert o["bad"] == [0] * 6, (r, o["bad"])
 
 
 def test_schedules_interleaved_on_one_communicator(dev):
@@ -412,6 +457,7 @@ def test_allreduce_8_ranks_full_size(dev, dtype, algos, gib, knobs):
     for r in range(n):
         assert "error" not in out[r], f"rank {r}:\n{out[r]['error']}"
         assert out[r]["destroy"] == 0
+        _check_placement(r, n, out[r]["info"], env)
         for res in out[r]["results"]:
             assert res["rc"] == 0 and res["async"] == 0, (r, res["algo"], res["rc"], res["async"])
             assert res["last_algo"] == res["algo"], (r, res["algo"], res["last_algo"])

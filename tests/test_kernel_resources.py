@@ -67,3 +67,25 @@ def test_collective_kernels_fit_two_waves_per_simd_without_scratch(tmp_path):
     assert not over, f"collective kernels above 256 registers (1 wave per SIMD): {over}"
     spill = {k: v for k, v in ks.items() if v["private_segment_fixed_size"] != 0}
     assert not spill, f"kernels using scratch memory: {spill}"
+
+
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)), reason="library not built / no llvm-objdump")
+def test_buffer_accesses_are_range_checked_on_their_whole_offset(tmp_path):
+    # read_fold_all issues the next batch's loads unconditionally -- up to two batches
+    # past the end of a slice, and so, for the last slice of a peer's chunk, past the end of the
+    # peer's mapped allocation.  They touch no memory only because a raw buffer access whose
+    # offset is at or past the resource's num_records returns 0 / stores nothing.  On gfx9 that
+    # range check covers voffset + the instruction's immediate offset but NOT soffset: an access
+    # the compiler had split into a uniform soffset part would escape it.  Every buffer load and
+    # store the library ships passes soffset 0 (kernels.hip hands its whole offset to voffset).
+    co = tmp_path / "co.elf"
+    co.write_bytes(_gfx950_code_object(LIB))
+    asm = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", str(co)], capture_output=True, text=True, check=True).stdout
+    ops = [ln.split("//")[0].split() for ln in asm.splitlines() if re.match(r"\s+buffer_(load|store)_", ln)]
+    assert len(ops) > 10000, len(ops)  # every kernel's buffer accesses were found
+    # operands: vdata, vaddr, srsrc, soffset [, modifiers]
+    bad = [" ".join(o) for o in ops if o[4].rstrip(",") != "0"]
+    assert not bad, f"buffer accesses with a non-zero soffset (outside the range check): {bad[:5]}"

@@ -270,3 +270,34 @@ def test_read_small_calls_run_only_the_pipelines_they_need(oracle_lib, sim_lib, 
     for seed in range(3):
         got, _ = S.allreduce(xs, slice_bytes=64, channels=C, algos=[2, 0, 2, 3, 2, 2, 0, 3, 2], seed=seed + 1)
         assert all(same_bits(g, e) for g, e in zip(got, ref))
+
+
+def _topo(n, kind=S.XGMI, hops=1, devices=None):
+    """n x n link / hop matrices: every pair over `kind` at `hops`, or, with `devices`, ranks on the
+    same device index reach each other through that GPU (SAME_GPU, 0 hops)"""
+    link = [[S.SAME_GPU if p == q or (devices and devices[p] == devices[q]) else kind for p in range(n)]
+            for q in range(n)]
+    hop = [[0 if link[q][p] == S.SAME_GPU else hops for p in range(n)] for q in range(n)]
+    return link, hop
+
+
+def test_topology_rule_for_the_default_schedule(sim_lib):
+    # VERDICT r4 #3: auto runs the read schedule only when every pair of ranks shares a GPU or is
+    # one xGMI hop apart (an MI355X node's full mesh; the co-located rehearsal), otherwise the
+    # ring -- decided from every rank's row, so every rank decides alike
+    assert S.topology_blocks_read(*_topo(8)) is None                               # the 8-GPU node
+    assert S.topology_blocks_read(*_topo(8, devices=[0] * 8)) is None              # 8 ranks, one GPU
+    assert S.topology_blocks_read(*_topo(4, devices=[0, 0, 1, 1])) is None         # 2 GPUs x 2 ranks
+    assert S.topology_blocks_read(*_topo(2, kind=S.PCIE)) == (0, 1)                # PCIe box
+    link, hops = _topo(8)
+    link[5][3] = S.PCIE                      # one peer of one rank over PCIe: the whole communicator
+    assert S.topology_blocks_read(link, hops) == (5, 3)
+    link, hops = _topo(8)
+    hops[2][6] = 2                           # xGMI but routed through another GPU
+    assert S.topology_blocks_read(link, hops) == (2, 6)
+    link, hops = _topo(3)
+    link[1][0] = S.UNKNOWN                   # a peer GPU that rank 1's process cannot see
+    assert S.topology_blocks_read(link, hops) == (1, 0)
+    # the diagonal (a rank and itself) never counts
+    link, hops = _topo(3, kind=S.PCIE, devices=[0, 0, 0])
+    assert S.topology_blocks_read(link, hops) is None
