@@ -191,13 +191,17 @@ SWEEP_POINTS = [
     ("ring", {}), ("ring", {"MINI_NCCL_SLOTS": 4}), ("ring", {"MINI_NCCL_SLICE_SIZE": 524288}),
     ("ring", {"MINI_NCCL_SYS_FENCE": 1}),
 ]
-ALGO_IDS = {"ring": 0, "read": 2}  # mncclAlgo_t
+ALGO_IDS = {"ring": 0, "read": 2, "read_grid": 4}  # mncclAlgo_t
+RAN_AS = {"ring": 0, "read": 2, "read_grid": 2}    # mncclCommInfo_t.last_algo of each (the grid form is read)
 ALGO_NAMES = {v: k for k, v in ALGO_IDS.items()}
 
 
 def kernel_form(algo, read_push=1):
-    """The kernel a schedule launches: ring_kernel, or read_kernel in its push / load form
-    (template PUSH): what a PMC entry must have profiled to describe this line's kernel."""
+    """The kernel a schedule launches: ring_kernel, read_kernel in its push / load form (template
+    PUSH), or the push form's grid launches (read_grid_kernel): what a PMC entry must have profiled
+    to describe this line's kernel."""
+    if algo == "read_grid":
+        return "read_grid"
     return "ring" if algo == "ring" else ("read_push" if read_push else "read_load")
 
 
@@ -208,7 +212,7 @@ def fused_bytes(form, esz, chunk, n):
     push form, every chunk of the input read once (n - 1 of them by the peers) and every chunk of
     the output written once (n - 1 of them by the peers' pushes): 2n; load form, the rank's own
     result chunk is also read back by the n - 1 peers: 3n - 1."""
-    k = {"ring": 6 * n - 4, "read_push": 2 * n, "read_load": 3 * n - 1}[form]
+    k = {"ring": 6 * n - 4, "read_push": 2 * n, "read_grid": 2 * n, "read_load": 3 * n - 1}[form]
     return esz * chunk * k
 C4_SLICES = [65536, 131072, 262144, 1048576]
 C4_WINDOWS = [16, 32, 64]
@@ -246,7 +250,7 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
         ok = comm.async_error() == 0 and bool((recv == float(n)).all().item())
         ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, st, 1, dist.barrier)
         i = comm.info()
-        ok = ok and i["last_algo"] == ALGO_IDS[algo]  # the point ran its own schedule
+        ok = ok and i["last_algo"] == RAN_AS[algo]  # the point ran its own schedule
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
         return {"GBps": round(count * esz / (dt / reps) / 1e9, 2), "ok": ok, "workgroups": i["channels"],
                 "pipelines": i["pipelines"], "slot_bytes": i["slot_bytes"], "scratch_MiB": i["scratch_bytes"] >> 20}
@@ -710,7 +714,8 @@ def main():
     ap.add_argument("--count", type=int, default=0, help="elements (default: 1 GiB of --dtype)")
     ap.add_argument("--dtype", choices=["f32", "bf16", "f16"], default="f32",
                     help="f32 = the headline; bf16/f16 = BASELINE.json configs[4] (C5)")
-    ap.add_argument("--algo", choices=["auto", "ring", "read"], default=os.environ.get("MINI_NCCL_ALGO", "auto"),
+    ap.add_argument("--algo", choices=["auto", "ring", "read", "read_grid"],
+                    default=os.environ.get("MINI_NCCL_ALGO", "auto"),
                     help="auto = the library default (read for device buffers; same bits whatever the schedule)")
     ap.add_argument("--no-alt", action="store_true", help="skip the extras: N>1 the second schedule and the RCCL reference, N=1 the host-inclusive rate")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -892,6 +897,7 @@ def main():
         def run_algo(algo, auto=False):
             comm.set_algo(M.ALGO_AUTO if auto else ALGO_IDS[algo])
             inject(f"run_{algo}")
+            grid0 = comm.info()["read_grid_calls"]
             step = make_step()
             recv.fill_(-1.0)
             for _ in range(max(1, args.warmup)):
@@ -916,11 +922,14 @@ def main():
                                                "element" + ("" if ok else ": FAILED")}
             ok = ok and order == "ok"
             i = comm.info()
-            ran_ok = i["last_algo"] == ALGO_IDS[algo]  # the timed calls ran this schedule (no fallback)
+            ran_ok = i["last_algo"] == RAN_AS[algo]  # the timed calls ran this schedule (no fallback)
+            if algo == "read_grid":  # every call of the point (warm-up, timed, checks) in the grid form
+                ran_ok = ran_ok and i["read_grid_calls"] - grid0 >= max(1, args.warmup) + args.steps
             if not ran_ok:
                 # e.g. the read schedule could not map a peer's buffers on this node and the calls
                 # ran the ring: on record in the line, not only as a FAILED check
                 fallbacks[algo] = {"rank": rank, "ran": {0: "ring", 2: "read", 3: "oneshot"}.get(i["last_algo"], "?"),
+                                   "grid_calls": i["read_grid_calls"] - grid0,
                                    "read_map_failures": i["read_map_failures"],
                                    "ipc_open_failures": i["ipc_open_failures"], "cap_refusals": i["cap_refusals"]}
                 log(f"rank {rank}: {algo} calls ran {fallbacks[algo]['ran']}: {fallbacks[algo]}")
@@ -1043,7 +1052,7 @@ def main():
             arm(result)
         # 3. the other schedules on the same buffers (same bits), each its own labelled point
         if not args.no_alt:
-            for other in ("ring", "read"):
+            for other in ("ring", "read", "read_grid"):
                 if other in result["schedules"]:
                     continue
                 if rank == 0:
@@ -1064,6 +1073,12 @@ def main():
                         "same bits); otherwise this node should run MINI_NCCL_ALGO=ring",
                 "read_GBps": rd["value"], "ring_GBps": rg["value"], "read_over_ring": round(rd["value"] / rg["value"], 3),
                 "holds": rd["value"] >= rg["value"]}
+            gd = result["schedules"].get("read_grid", {})
+            if "value" in gd:
+                # the grid form (mncclAlgoReadGrid), measured beside on the same buffers: if it wins on
+                # the node, it is the candidate for the default there
+                result["config"]["headline_check"].update({"read_grid_GBps": gd["value"],
+                                                           "read_grid_over_read": round(gd["value"] / rd["value"], 3)})
         if rank == 0:
             arm(result)
         # 4. the xGMI roofline the schedules are bound by, after the schedules themselves: bytes

@@ -34,7 +34,7 @@ extern "C" {
    401 the one-shot schedule (mncclAlgoOneShot; auto's small calls that would run the ring);
    500 auto runs the read schedule only where every pair of GPUs is one xGMI hop apart (or
    shares a GPU), mncclCommInfo_t grew (same prefix: auto_read, peer_link / peer_hops,
-   auto_reason) */
+   auto_reason, read_grid_calls), mncclAlgoReadGrid */
 #define MNCCL_VERSION 500
 
 /* schedules; all produce bit-identical results (same fold order per element) */
@@ -62,7 +62,12 @@ typedef enum {
                           2(n-1).  mncclAlgoAuto takes it for calls of at most 64 KiB that the
                           read schedule cannot take (host buffers, a full export table); forced,
                           every call whose pieces fit one round of the pipelines (the others run
-                          as with mncclAlgoAuto) */
+                          as with mncclAlgoAuto) */,
+  mncclAlgoReadGrid = 4 /* since 500: mncclAlgoRead with its large calls (chunks of >= 4 MiB, whole
+                           16-byte vectors, up to 8 ranks, push form) launched as a one-wave START,
+                           a grid of one-batch fold workgroups and a one-wave DONE instead of the
+                           persistent kernel; the same bits.  A runtime form for the node to
+                           measure beside the default (mncclCommInfo_t.read_grid_calls) */
 } mncclAlgo_t;
 
 typedef struct {
@@ -116,6 +121,8 @@ typedef struct {
                                             type (hipExtGetLinkTypeAndHopCount: 2 PCIe, 4 xGMI) */
   int peer_hops[16];                     /* hop count of that link (0 for the same GPU) */
   char auto_reason[160];                 /* the rule's verdict in words (NUL-terminated) */
+  unsigned long long read_grid_calls;    /* calls this communicator ran in the read schedule's grid
+                                            form (mncclAlgoReadGrid) */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,

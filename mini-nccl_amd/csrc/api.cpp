@@ -192,6 +192,7 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
     info->peer_hops[q] = q < c->nranks() ? c->peer_hops(q) : 0;
   }
   snprintf(info->auto_reason, sizeof info->auto_reason, "%s", c->topology_reason().c_str());
+  info->read_grid_calls = c->read_grid_calls();
   memcpy(out, &full, size < sizeof full ? size : sizeof full);
   return ncclSuccess;
 }
@@ -201,7 +202,8 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
 ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo) {
   if (!comm) return ncclInvalidArgument;
   // mncclAlgoDirect (1) was removed in 400: it never beat the ring on any measured setup
-  if (algo != mncclAlgoRing && algo != mncclAlgoRead && algo != mncclAlgoOneShot && algo != mncclAlgoAuto)
+  if (algo != mncclAlgoRing && algo != mncclAlgoRead && algo != mncclAlgoOneShot && algo != mncclAlgoReadGrid &&
+      algo != mncclAlgoAuto)
     return ncclInvalidArgument;
   reinterpret_cast<Comm*>(comm)->set_algo(algo);
   return ncclSuccess;

@@ -149,6 +149,7 @@ void Comm::setup_device_resources() {
     // + the kernels' claim word (kernels.h CollParams::claim) in its own 256 bytes after them
     hip_check(hipMalloc((void**)&pair_seq_, seq_bytes + 256), "alloc pair_seq");
     claim_ = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(pair_seq_) + seq_bytes);
+    go_ = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(pair_seq_) + seq_bytes + 128);
     // zeroed on a private stream: a device-wide sync (or the legacy null stream) would also wait
     // for other communicators' persistent kernels in this process, which may be waiting for us
     hipStream_t st = nullptr;
@@ -384,6 +385,7 @@ void Comm::release() {
   mbox_ = nullptr;
   pair_seq_ = nullptr;
   claim_ = nullptr;
+  go_ = nullptr;
   h_ctl_ = nullptr;
   (void)hipGetLastError();
 }
@@ -553,12 +555,18 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.read_push = cfg_.read_push;
   p.tail_bytes = tail_bytes;
   p.claim = claim_;
+  p.go = go_;
   const int nt = cfg_.threads, wg = A / geo_.waves;
-  hipError_t e = algo == 2   ? launch_read(dtype, op, vec, wg, nt, p, stream)
+  // mncclAlgoReadGrid: the push form's large calls as start / grid fold / done (the same on every
+  // rank: the schedule, the push form, vec and the size are rank-uniform)
+  const bool grid = algo == 2 && algo_ == 4 && cfg_.read_push && vec && read_grid_fits(chunk_bytes, n);
+  hipError_t e = grid        ? launch_read_grid(dtype, op, p, stream)
+                 : algo == 2 ? launch_read(dtype, op, vec, wg, nt, p, stream)
                  : algo == 3 ? launch_oneshot(dtype, op, vec, wg, nt, p, stream)
                              : launch_ring(dtype, op, vec, wg, nt, p, stream);
   hip_check(e, "kernel launch");
   last_algo_ = algo;
+  if (grid) ++read_grid_calls_;
 }
 
 ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t stream) {
@@ -618,8 +626,9 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     const bool small = auto_ && oneshot_fits(chunk_bytes, n, wave_channels(), wave_slice(), false);
     // (auto, and a forced one-shot's larger calls, only where the topology allows the read
     // schedule: classify_topology; MINI_NCCL_ALGO=read forces it anywhere)
-    const bool read_sched =
-        !oneshot && ((algo_ == 2 && (!auto_ || topo_read_)) || (algo_ == 3 && topo_read_)) && pbuf_.available();
+    const bool read_sched = !oneshot &&
+                            (((algo_ == 2 || algo_ == 4) && (!auto_ || topo_read_)) || (algo_ == 3 && topo_read_)) &&
+                            pbuf_.available();
     if (read_sched) pbuf_.reap(send, recv);
     const Reach rs = read_sched && pbuf_.known(send) ? (local_s = true, Reach::kDevice) : reach(send, &ksend, &local_s);
     const Reach rr = read_sched && pbuf_.known(recv) ? (local_r = true, Reach::kDevice)

@@ -34,12 +34,14 @@ class Comm {
   const Config& config() const { return cfg_; }
   int algo() const { return auto_ ? -1 : algo_; }
   // a < 0: the default (read for buffers every rank can share; for the other calls the one-shot
-  // when small, else the ring); 0 ring, 2 read, 3 one-shot wherever a call fits it
+  // when small, else the ring); 0 ring, 2 read, 3 one-shot wherever a call fits it, 4 read with
+  // its large calls in the grid form (kernels.hip read_grid_kernel)
   void set_algo(int a) {
     auto_ = a < 0;
     algo_ = a < 0 ? 2 : a;
   }
   int last_algo() const { return last_algo_; }  // schedule of the last launched kernel, -1: none
+  unsigned long long read_grid_calls() const { return read_grid_calls_; }  // calls run in the grid form
   size_t peer_mappings() const { return pbuf_.mapped_allocations(); }
   const PeerBuffers& peer_buffers() const { return pbuf_; }
   // rank processes / communicators whose GPU is this rank's GPU (this rank included)
@@ -89,6 +91,7 @@ class Comm {
                                  // buffers cannot be shared), 3 one-shot (larger calls: as auto)
   bool auto_ = true;             // the default: as algo_ = 2, with the ring's small calls one-shot
   int last_algo_ = -1;
+  unsigned long long read_grid_calls_ = 0;  // read calls launched as start / grid / done
   int ranks_on_device_ = 1;
   bool topo_read_ = true;        // auto may run the read schedule (every pair: same GPU or 1 xGMI hop)
   std::string topo_why_ = "read: one rank";
@@ -102,6 +105,7 @@ class Comm {
   size_t mbox_bytes_ = 0;
   uint64_t* pair_seq_ = nullptr; // [2][n][C]: per (peer, channel) tx / rx message counters (device)
   uint32_t* claim_ = nullptr;    // after them: the kernels' first-give-up word (kernels.h)
+  uint32_t* go_ = nullptr;       // and the grid form's START-through word (kernels.h CollParams::go)
   uint32_t* h_ctl_ = nullptr;    // host-mapped: [0] status, [1] abort request, [2] last started call
   uint32_t* d_ctl_ = nullptr;    // device view of h_ctl_
 

@@ -88,10 +88,11 @@ Config Config::from_env() {
     if (!strcmp(a, "ring")) c.algo = 0;
     else if (!strcmp(a, "read")) c.algo = 2;
     else if (!strcmp(a, "oneshot")) c.algo = 3;
+    else if (!strcmp(a, "read_grid")) c.algo = 4;
     else if (!strcmp(a, "auto")) c.algo = -1;
     else if (!strcmp(a, "direct"))  // round 1-3's third schedule: never faster than the ring, removed in 4.0
       throw std::invalid_argument("MINI_NCCL_ALGO=direct is no longer built (4.0): use auto, ring, read or oneshot");
-    else throw std::invalid_argument(std::string("MINI_NCCL_ALGO=") + a + " (expected auto|ring|read|oneshot)");
+    else throw std::invalid_argument(std::string("MINI_NCCL_ALGO=") + a + " (expected auto|ring|read|oneshot|read_grid)");
   }
   c.blocking = env_int("MINI_NCCL_BLOCKING", 1) != 0;
   c.sys_fence = env_int("MINI_NCCL_SYS_FENCE", 0) != 0;
@@ -110,7 +111,8 @@ std::string Config::describe() const {
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, scratch_cap=%zu MiB, algo=%s, "
            "blocking=%d, sys_fence=%d, read_push=%d, timeout=%.0f ms, port=%d",
            slice_size, window_size, signal_batch, slots, channels, threads, scratch_cap >> 20,
-           algo < 0 ? "auto" : algo == 2 ? "read" : algo == 3 ? "oneshot" : "ring", blocking, sys_fence, read_push, timeout_ms, port);
+           algo < 0 ? "auto" : algo == 2 ? "read" : algo == 3 ? "oneshot" : algo == 4 ? "read_grid" : "ring", blocking,
+           sys_fence, read_push, timeout_ms, port);
   return b;
 }
 

@@ -40,6 +40,8 @@ struct CollParams {
                               // (the reference leaves them as its copy made them, api.cpp:173-175)
   uint32_t* claim;            // device word, 0 until the communicator's first give-up claims it:
                               // only that lane writes the status and its diagnostic
+  uint32_t* go;               // device word: the read schedule's grid form -- call_seq once START
+                              // is through (read_start_kernel), checked by the grid and DONE launches
 };
 
 constexpr int kMaxRanks = 16;
@@ -52,6 +54,9 @@ hipError_t launch_read(int dtype, int op, bool vec, int channels, int threads,
                        const CollParams& p, hipStream_t stream);
 hipError_t launch_oneshot(int dtype, int op, bool vec, int channels, int threads,
                           const CollParams& p, hipStream_t stream);
+// the read schedule's push form for large calls as three launches (start, grid fold, done):
+// schedule.h read_grid_fits(p.chunk_bytes, p.n) (2 <= n <= 8, whole 16-byte vectors), p.go set
+hipError_t launch_read_grid(int dtype, int op, const CollParams& p, hipStream_t stream);
 // out[i] = op(local[i], incoming[i]) for i < count
 hipError_t launch_local_reduce(int dtype, int op, void* out, const void* local,
                                const void* incoming, uint64_t count, hipStream_t stream);

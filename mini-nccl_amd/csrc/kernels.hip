@@ -11,6 +11,9 @@
 //  read_kernel    the default: same association order, no scratch -- each rank loads its
 //                 peers' send buffers over the links and pushes its results into their recv
 //                 buffers (mapped by Comm per allocation).
+//  read_start / read_grid / read_done   the read schedule's push form as three launches (the
+//                 runtime form mncclAlgoReadGrid, for large calls): a grid of one-batch workgroups
+//                 between a one-wave START and a one-wave DONE.
 //  oneshot_kernel small calls the read schedule cannot take (host buffers): one hand-off -- every
 //                 rank stores its pieces into every peer's scratch and folds the result itself,
 //                 same association order.
@@ -882,6 +885,104 @@ aborted:
     for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), abort_word(p));
 }
 
+// ---------------------------------------------------------------- read schedule, grid form
+// mncclAlgoReadGrid / MINI_NCCL_ALGO=read_grid (a runtime form, not the default): the push form of
+// a large call (schedule.h read_grid_fits) as three launches on the call's stream --
+// read_start_kernel (one wave, pipeline 0: START to every peer, wait for theirs, then the device
+// word `go` = this call), read_grid_kernel (the fold with no flag in sight: one one-wave
+// workgroup per 1 KiB of my chunk, dispatched in address order, gone when done) and
+// read_done_kernel (one wave: DONE to every peer, wait for theirs).  Why: the persistent kernel's
+// long-lived waves move a 1:1 read:write stream at 72-80 % of HBM depending on where the buffers
+// landed physically, while the dispatcher's one-batch workgroups held 77-81 % on every placement
+// (tools/mix_probe.hip, profiles/r4_mix_probe_alloc.txt); on the one-GPU proxy it was 1.05x the
+// persistent form at 2 ranks but 0.63x at 8 co-located ranks (profiles/r4_read_grid_ab.txt) --
+// which a node, one rank per GPU, never has -- so the node's bench measures both
+// (schedules.read_grid).  The protocol is the push form's with one pipeline and one iteration
+// (START, DONE: read_msgs_per_call(1) messages on pipeline 0's counters), which the simulator
+// checks for a one-slice read call.  Stream order does the rest: the grid starts after START is
+// through (its workgroups still check `go`: after a failed START they must not touch a peer's
+// buffers), and every wave drains its stores before it ends, so when DONE is raised every load of
+// a peer's send has returned and every push has been acknowledged by the peer's memory.
+__global__ void __launch_bounds__(64) read_start_kernel(CollParams p) {
+  signal_start(p);
+  const int lane = threadIdx.x, n = p.n, r = p.rank, C = p.pipes;
+  copy_tail(p, 0, lane);
+  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox, p.claim};
+  const bool peer = lane < n && lane != r;
+  const u64 tx = peer ? p.tx_seq[(u64)lane * C] : 0, rx = peer ? p.rx_seq[(u64)lane * C] : 0;
+  if (peer) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, 0), tx + 1);
+  const bool ok = wave_wait_peers(p.mbox + mbox_ready(C, lane, 0), rx + 1, peer, ctl, lane, true);
+  // 0 after a failed START (a graph replay reuses call_seq: the word must not keep a stale "go")
+  if (lane == 0) *p.go = ok ? p.call_seq : 0u;
+  if (!ok && lane == 0)
+    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), abort_word(p));
+}
+
+// one batch of V vectors per lane of my chunk: the peers' slices of it loaded together (G peer
+// slots, as read_fold_all), folded in ring order, stored into my recv and pushed into every
+// peer's recv (the push order rotated by workgroup so the workgroups' stores spread over the links)
+template <typename T, int OPC, int G, int V>
+__global__ void __launch_bounds__(64) read_grid_kernel(CollParams p) {
+  if (*p.go != p.call_seq) return;  // START failed: the peers' buffers are not ours to touch
+  constexpr uint32_t B = 64u * 16u * V;
+  const uint64_t off = (uint64_t)blockIdx.x * B;
+  if (off >= p.chunk_bytes) return;
+  const int n = p.n, r = p.rank, lane = threadIdx.x;
+  const uint32_t len = (uint32_t)(p.chunk_bytes - off < B ? p.chunk_bytes - off : B);
+  const uint64_t coff = (uint64_t)r * p.chunk_bytes + off;
+  const rsrc_t loc = make_rsrc(p.send + coff, len), out = make_rsrc(p.recv + coff, len);
+  v4u x[G][V], a[V];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+    if (g + 1 < n) {
+      const rsrc_t in = make_rsrc(p.peer_send[direct_peer(n, r, 1 + g)] + coff, len);
+#pragma unroll
+      for (int u = 0; u < V; ++u) x[g][u] = ld_slot16(in, (uint32_t)(u * 64 + lane) * 16);
+    }
+#pragma unroll
+  for (int u = 0; u < V; ++u) a[u] = ld_nt16(loc, (uint32_t)(u * 64 + lane) * 16);
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+    if (g + 1 < n) {
+#pragma unroll
+      for (int u = 0; u < V; ++u) a[u] = reduce16<T, OPC>(x[g][u], a[u]);
+    }
+#pragma unroll
+  for (int u = 0; u < V; ++u) st_slot16(out, (uint32_t)(u * 64 + lane) * 16, a[u]);
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+    if (g + 1 < n) {
+      const int q = direct_peer(n, r, 1 + (int)((g + blockIdx.x) % (unsigned)(n - 1)));
+      const rsrc_t po = make_rsrc(p.peer_recv[q] + coff, len);
+#pragma unroll
+      for (int u = 0; u < V; ++u) st_slot16(po, (uint32_t)(u * 64 + lane) * 16, a[u]);
+    }
+  drain_stores();  // every push acknowledged by the peer's memory before this wave ends
+}
+
+__global__ void __launch_bounds__(64) read_done_kernel(CollParams p) {
+  if (*p.go != p.call_seq) return;  // START failed and already raised the peers' ABORT words
+  const int lane = threadIdx.x, n = p.n, r = p.rank, C = p.pipes;
+  const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox, p.claim};
+  const bool peer = lane < n && lane != r;
+  const u64 mpc = read_msgs_per_call(1);
+  const u64 tx = peer ? p.tx_seq[(u64)lane * C] : 0, rx = peer ? p.rx_seq[(u64)lane * C] : 0;
+  if (p.sys_fence && lane == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (peer) {
+    st_sys(p.peer_mbox[lane] + mbox_credit(n, C, r, 0), rx + mpc);
+    st_sys(p.peer_mbox[lane] + mbox_ready(C, r, 0), tx + mpc);
+  }
+  if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, 0), rx + mpc, peer, ctl, lane, false)) {
+    if (lane == 0)
+      for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), abort_word(p));
+    return;
+  }
+  if (peer) {
+    p.tx_seq[(u64)lane * C] = tx + mpc;
+    p.rx_seq[(u64)lane * C] = rx + mpc;
+  }
+}
+
 // ---------------------------------------------------------------- one-shot kernel
 // Small calls (schedule.h oneshot_fits): one hand-off instead of the ring's 2(n-1) dependent
 // ones.  Pipeline w = s * n + c owns slice s of chunk c: it stores that piece of its send into
@@ -1198,6 +1299,43 @@ static hipError_t oneshot_for_t(int op, bool vec, int C, int nt, const CollParam
     default: return hipErrorInvalidValue;
   }
 #undef ONESHOT_CASE
+  return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t read_grid_for_t(int op, const CollParams& p, hipStream_t st) {
+  const unsigned blocks = (unsigned)((p.chunk_bytes + 1023) / 1024);  // V = 1: 1 KiB per workgroup
+  const int n = p.n;
+#define GRID_G(OPC, G) hipLaunchKernelGGL((read_grid_kernel<T, OPC, G, 1>), dim3(blocks), dim3(64), 0, st, p)
+#define GRID_CASE(OPC)                    \
+  case OPC:                               \
+    if (n == 2) GRID_G(OPC, 1);           \
+    else if (n == 3) GRID_G(OPC, 2);      \
+    else if (n <= 5) GRID_G(OPC, 4);      \
+    else GRID_G(OPC, 7);                  \
+    break;
+  switch (op) {
+    GRID_CASE(kSum) GRID_CASE(kProd) GRID_CASE(kMax) GRID_CASE(kMin)
+    default: return hipErrorInvalidValue;
+  }
+#undef GRID_CASE
+#undef GRID_G
+  return hipGetLastError();
+}
+
+hipError_t launch_read_grid(int dtype, int op, const CollParams& p, hipStream_t st) {
+  // the shapes the grid kernel assumes, checked before anything is launched
+  if (p.n < 2 || p.n > 8 || p.chunk_bytes % 16 || !p.go || !read_grid_fits(p.chunk_bytes, p.n) ||
+      (p.chunk_bytes + 1023) / 1024 > 0x7fffffffull)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(read_start_kernel, dim3(1), dim3(64), 0, st, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+#define M(T) e = read_grid_for_t<T>(op, p, st)
+  MNCCL_DISPATCH_T(dtype, M)
+#undef M
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(read_done_kernel, dim3(1), dim3(64), 0, st, p);
   return hipGetLastError();
 }
 

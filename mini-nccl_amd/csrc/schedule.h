@@ -170,6 +170,17 @@ MNCCL_HD bool oneshot_fits(uint64_t chunk_bytes, int n, int C, uint64_t slot_byt
   return sl <= slot_bytes && (chunk_bytes + sl - 1) / sl * (uint64_t)n <= (uint64_t)C;
 }
 
+// The read schedule's grid form (mncclAlgoReadGrid; kernels.hip read_grid_kernel): three launches
+// instead of the persistent kernel -- a one-wave START, a grid of one-batch workgroups that only
+// fold and push, a one-wave DONE -- with the protocol of a one-slice read call on pipeline 0.
+// Chunks of at least kReadGridMin bytes, whole 16-byte vectors, up to 8 ranks (the fold's peer
+// groups); smaller or ragged calls run the persistent read kernel.  Measured in
+// profiles/r4_read_grid_ab.txt.
+constexpr uint64_t kReadGridMin = 4ull << 20;
+MNCCL_HD bool read_grid_fits(uint64_t chunk_bytes, int n) {
+  return n >= 2 && n <= 8 && chunk_bytes >= kReadGridMin && chunk_bytes % 16 == 0;
+}
+
 // Scratch layout: one region per PEER rank (n - 1 of them: the owner never sends to itself),
 // [C][slots][slice_bytes] each.  region_index maps a peer rank q != owner to its region.
 MNCCL_HD uint64_t scratch_region_bytes(int C, int slots, uint64_t slice_bytes) { return (uint64_t)C * slots * slice_bytes; }

@@ -36,7 +36,7 @@ ncclFloat16, ncclFloat, ncclDouble, ncclBfloat16 = 6, 7, 8, 9
 ncclSum, ncclProd, ncclMax, ncclMin, ncclAvg = 0, 1, 2, 3, 4
 
 # mncclAlgo_t (mncclAlgoDirect = 1 was removed in mncclVersion 400)
-ALGO_AUTO, ALGO_RING, ALGO_READ, ALGO_ONESHOT = -1, 0, 2, 3
+ALGO_AUTO, ALGO_RING, ALGO_READ, ALGO_ONESHOT, ALGO_READ_GRID = -1, 0, 2, 3, 4
 
 DTYPE_SIZE = {ncclInt32: 4, ncclFloat16: 2, ncclFloat: 4, ncclDouble: 8, ncclBfloat16: 2}
 
@@ -58,7 +58,7 @@ class CommInfo(ctypes.Structure):
         ("cap_refusals", ctypes.c_ulonglong), ("liveness_queries", ctypes.c_ulonglong), ("read_push", ctypes.c_int),
         # since mncclVersion 500
         ("auto_read", ctypes.c_int), ("peer_link", ctypes.c_int * 16), ("peer_hops", ctypes.c_int * 16),
-        ("auto_reason", ctypes.c_char * 160),
+        ("auto_reason", ctypes.c_char * 160), ("read_grid_calls", ctypes.c_ulonglong),
     ]
 
 

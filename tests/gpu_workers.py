@@ -124,6 +124,7 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
             if not inplace:
                 recv.fill_byte(0xAB)
             rc = 0
+            grid0 = comm.info()["read_grid_calls"]
             t0 = time.time()
             bad, first, detail = 0, -1, ""
             # "vary": new inputs every call, each call checked (a stale slot or flag from the
@@ -161,6 +162,7 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
             ci = comm.info()
             results.append({"case": case, "rc": rc, "bad": bad, "first": first, "detail": detail, "secs": dt,
                             "async": comm.async_error(), "last_algo": ci["last_algo"],
+                            "grid_calls": ci["read_grid_calls"] - grid0,
                             "peer_mappings": ci["peer_mappings"], "ipc_open_failures": ci["ipc_open_failures"],
                             "read_map_failures": ci["read_map_failures"], "closed_freed": ci["closed_freed"],
                             "live_exports": ci["live_exports"]})
@@ -394,12 +396,13 @@ def graph_rank(rank, n, port, env, replays, out_q):
         use_rank_device(rank)
         comm = M.Comm(n, rank, "127.0.0.1")
         st = hip_rt.Stream()
-        count = (1 << 18) + 1
+        count = int(env.get("GRAPH_COUNT", (1 << 18) + 1))
         send, recv = hip_rt.DeviceBuffer(count * 4), hip_rt.DeviceBuffer(count * 4)
         rcs = []
         g = hip_rt.Graph(st, lambda: rcs.append(comm.all_reduce(send.ptr, recv.ptr, count, M.ncclFloat, M.ncclSum,
                                                                 st.handle)))
         captured_algo = comm.info()["last_algo"]  # the schedule baked into the graph
+        captured_grid = comm.info()["read_grid_calls"]
         bad = []
         for k in range(replays):
             xs = O.random_inputs(n, count, "f32", seed=500 + k)
@@ -418,6 +421,7 @@ def graph_rank(rank, n, port, env, replays, out_q):
         exp = O.allreduce(xs, "f32", "sum")[rank]
         g.destroy()
         out_q.put((rank, {"capture_rc": rcs, "bad": bad, "eager_rc": rc, "captured_algo": captured_algo,
+                          "captured_grid": captured_grid,
                           "eager_bad": int((got.view(np.uint32) != exp.view(np.uint32)).sum())}))
         send.free()
         recv.free()

@@ -100,13 +100,15 @@ def _run_allreduce(n, cases, env=None, timeout=300, barrier=True):
             # the read schedule ran (no fallback) whenever every rank's buffers are device memory,
             # fresh allocations at re-used addresses included (dma-buf exports, csrc/ipcreg.h)
             dev_bufs = all(c.get(k, "device") == "device" for k in ("mem", "recv_mem"))
-            if c["algo"] == 2 and dev_bufs and c["count"] >= n:
+            if c["algo"] in (2, 4) and dev_bufs and c["count"] >= n:
                 assert res["last_algo"] == 2, f"rank {r} case {c}: ran schedule {res['last_algo']}"
             # forced one-shot: every case of the tests below fits it
             if c["algo"] == 3 and c["count"] >= n:
                 assert res["last_algo"] == 3, f"rank {r} case {c}: ran schedule {res['last_algo']}"
             if "expect_algo" in c:
                 assert res["last_algo"] == c["expect_algo"], f"rank {r} case {c}: ran schedule {res['last_algo']}"
+            if "expect_grid" in c:  # the read schedule's grid form ran every call of the case (or none)
+                assert res["grid_calls"] == (c["calls"] if c["expect_grid"] else 0), (r, c, res["grid_calls"])
             # no IPC open ever failed (nothing retries: a failure would send a call to the
             # ring, csrc/peerbuf.cpp), in this process or in any rank's mapping round
             assert res["ipc_open_failures"] == 0 and res["read_map_failures"] == 0, (r, c, res)
@@ -317,6 +319,37 @@ def test_read_push_visible_to_cached_consumers(dev, n, algo, env):
         assert o["rcs"] == [0] * 6 and o["async"] == 0 and o["destroy"] == 0, o
         assert o["algos"] == [algo] * 6, o["algos"]
         assert o["bad"] == [0] * 6, (r, o["bad"])
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+def test_read_grid_parity(dev, n):
+    # mncclAlgoReadGrid, the push form's large calls as start / grid fold / done
+    # launches (chunks >= 4 MiB, whole 16-byte vectors): ring-order bits vs the oracle, tails, in
+    # place, 2-byte types, every op, repeated calls on varying data; a chunk just below the
+    # threshold and an odd one stay on the persistent kernel
+    m = 1 << 20  # 4 MiB of fp32 per chunk
+    g = 4        # mncclAlgoReadGrid
+    cases = [_case(count=n * m + n - 1, algo=g, seed=900, expect_grid=True, expect_algo=2),
+             _case(count=n * m, algo=g, seed=901, inplace=True, expect_grid=True),
+             _case(dtype="bf16", count=n * 2 * m + 1, algo=g, seed=902, expect_grid=True),
+             _case(dtype="f64", op="max", count=n * (m // 2) + n * 64, algo=g, seed=903, special=True, expect_grid=True),
+             _case(op="prod", count=n * (m + 4), algo=g, seed=904, calls=3, vary=True, expect_grid=True),
+             _case(dtype="i32", op="min", count=n * (m + 4) + 1, algo=g, seed=905, expect_grid=True),
+             _case(count=n * (m - 256), algo=g, seed=906, expect_grid=False, expect_algo=2),  # below 4 MiB
+             _case(dtype="f16", count=n * (2 * m + 1), algo=g, seed=907, expect_grid=False),  # chunk % 16 != 0
+             _case(count=n * m + 1, algo=-1, seed=908, expect_grid=False, expect_algo=2)]     # auto: persistent
+    _run_allreduce(n, cases, {"GPU_MAX_HW_QUEUES": "2"} if n > 4 else None, timeout=600)
+
+
+def test_read_grid_skewed_and_interleaved(dev):
+    # grid-form calls between persistent read, ring and one-shot calls on one communicator (the
+    # grid form moves pipeline 0's counters only), ranks entering every call out of step
+    n = 4
+    plan = [(4, n * (1 << 20)), (0, 70001), (2, 5000), (4, n * (1 << 20) + 3), (3, 3000), (4, n * (3 << 20)),
+            (2, n * (1 << 20))]
+    cases = [_case(count=c, algo=a, calls=2, vary=True, seed=950 + i, skew_ms=20, inplace=(i % 2 == 1))
+             for i, (a, c) in enumerate(plan)]
+    _run_allreduce(n, cases, timeout=600)
 
 
 def test_schedules_interleaved_on_one_communicator(dev):
@@ -536,12 +569,15 @@ def test_late_peer_is_aborted_fast(dev, algo):
     assert out[1]["secs"] < 1.5, out[1]  # well under its own 1.5 s watchdog + 2 s host limit
 
 
-@pytest.mark.parametrize("algo", ["ring", "read", "oneshot"])
+@pytest.mark.parametrize("algo", ["ring", "read", "oneshot", "read_grid"])
 def test_allreduce_hip_graph_capture_and_replay(dev, algo):
     # the reference only warns under capture (api.cpp:153-166); here a captured all-reduce
-    # replays correctly because the FIFO counters are device state advanced by the kernel
+    # replays correctly because the FIFO counters are device state advanced by the kernel (the
+    # grid form: three captured launches, its `go` word rewritten by every replay's START)
     port = GW.free_port()
     env = {"MINI_NCCL_TIMEOUT_MS": "20000", "MINI_NCCL_ALGO": algo}
+    if algo == "read_grid":
+        env["GRAPH_COUNT"] = str(3 * (1 << 20) + 1)
     out = GW.run_ranks(GW.graph_rank, 3, lambda r: (r, 3, port, env, 4), 240)
     assert sorted(out) == [0, 1, 2], out
     for r in range(3):
@@ -550,7 +586,8 @@ def test_allreduce_hip_graph_capture_and_replay(dev, algo):
         assert out[r]["bad"] == [0, 0, 0, 0]
         assert out[r]["eager_rc"] == 0 and out[r]["eager_bad"] == 0
         # the read schedule is captured too (its peer mappings pinned for the replays)
-        assert out[r]["captured_algo"] == {"ring": 0, "read": 2, "oneshot": 3}[algo]
+        assert out[r]["captured_algo"] == {"ring": 0, "read": 2, "oneshot": 3, "read_grid": 2}[algo]
+        assert out[r]["captured_grid"] == (1 if algo == "read_grid" else 0)
 
 
 @pytest.mark.parametrize("algo", ["ring", "read", "oneshot"])

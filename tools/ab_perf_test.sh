@@ -23,9 +23,9 @@ run() {
 }
 for round in 1 2 3; do
   for nr in ${NRS:-2 4}; do
-    for algo in ${ALGOS:-ring direct}; do
-      run $nr "A round=$round n=$nr algo=$algo" LD_LIBRARY_PATH=$AB_DIR MINI_NCCL_ALGO=$algo MINI_NCCL_TUNE=0
-      run $nr "B round=$round n=$nr algo=$algo" MINI_NCCL_ALGO=$algo MINI_NCCL_TUNE=0
+    for algo in ${ALGOS:-ring read}; do
+      run $nr "A round=$round n=$nr algo=$algo" LD_LIBRARY_PATH=$AB_DIR MINI_NCCL_ALGO=$algo
+      run $nr "B round=$round n=$nr algo=$algo" MINI_NCCL_ALGO=$algo
     done
   done
 done

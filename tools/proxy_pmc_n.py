@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""PMC passes of tools/r2_investigate.sh (gpurun_out/<tag>/{fetch,write}_<form>_n<N>) -> per-launch
+"""PMC passes of tools/historical/r2_investigate.sh or tools/r2_profile_read.sh (gpurun_out/<tag>/{fetch,write}_<form>_n<N>) -> per-launch
 HBM bytes of rank 0's kernel on the N-rank one-GPU proxy, with the gfx950 corrections (FETCH x2,
 KiB x1024, MI355X_MICROARCH.md), against the fused algorithmic bytes of its kernel form (bench.py
 fused_bytes: ring (6n-4) chunks, read_push 2n, read_load 3n-1), next to the kernel-trace durations.

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Read schedule (MINI_NCCL_ALGO=read): its GPU tests, then ring / direct / read on the one-GPU
+# Read schedule (MINI_NCCL_ALGO=read): its GPU tests, then ring / read on the one-GPU
 # proxy (2, 4, 8 rank processes, 1 GiB fp32 per rank; perf_test rank 0's row per point).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -31,7 +31,7 @@ run() {
 IFS=';' read -ra VARS <<< "${VARIANTS:-}"
 [ ${#VARIANTS} -eq 0 ] && VARS=("")
 for n in ${NRS:-2 4 8}; do
-  for a in ${ALGOS:-ring direct read}; do
+  for a in ${ALGOS:-ring read}; do
     for v in "${VARS[@]}"; do
       run $n "$a $v" MINI_NCCL_ALGO=$a $v
     done

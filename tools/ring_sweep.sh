@@ -20,7 +20,7 @@ run() {
   [ $rc -eq 124 ] || [ $rc -eq 137 ] && exit 9
   return 0
 }
-for algo in ${ALGOS:-ring direct}; do
+for algo in ${ALGOS:-ring read}; do
   for ch in 16 32 64 128; do
     for thr in 64 256 512; do
       for sl in 131072 262144 524288; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Slice-size sweep on ONE GPU (all ranks on GPU 0): perf_test rows at SIZE MiB for NR ranks,
-# ring and direct, MINI_NCCL_SLICE_SIZE in SLICES.  Protocol efficiency only, not xGMI.
+# ring and read, MINI_NCCL_SLICE_SIZE in SLICES.  Protocol efficiency only, not xGMI.
 SIZE=${SIZE:-1024}
 SLICES=${SLICES:-"16384 32768 65536 131072"}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -20,9 +20,9 @@ run() {
   return 0
 }
 for nr in ${NRS:-2 4 8}; do
-  for algo in ${ALGOS:-ring direct}; do
+  for algo in ${ALGOS:-ring read}; do
     for sl in $SLICES; do
-      run $nr "n=$nr algo=$algo slice=$sl" MINI_NCCL_ALGO=$algo MINI_NCCL_SLICE_SIZE=$sl MINI_NCCL_TUNE=0 ${EXTRA_ENV}
+      run $nr "n=$nr algo=$algo slice=$sl" MINI_NCCL_ALGO=$algo MINI_NCCL_SLICE_SIZE=$sl ${EXTRA_ENV}
     done
   done
 done
