@@ -34,7 +34,8 @@ extern "C" {
    401 the one-shot schedule (mncclAlgoOneShot; auto's small calls that would run the ring);
    500 auto runs the read schedule only where every pair of GPUs is one xGMI hop apart (or
    shares a GPU), mncclCommInfo_t grew (same prefix: auto_read, peer_link / peer_hops,
-   auto_reason, read_grid_calls), mncclAlgoReadGrid */
+   auto_reason, read_grid_calls, window_calls, windows), mncclAlgoReadGrid, registered windows
+   (mncclCommRegister / mncclCommDeregister: read calls with no host rendezvous) */
 #define MNCCL_VERSION 500
 
 /* schedules; all produce bit-identical results (same fold order per element) */
@@ -123,6 +124,8 @@ typedef struct {
   char auto_reason[160];                 /* the rule's verdict in words (NUL-terminated) */
   unsigned long long read_grid_calls;    /* calls this communicator ran in the read schedule's grid
                                             form (mncclAlgoReadGrid) */
+  unsigned long long window_calls;       /* calls launched on registered windows: no host rendezvous */
+  int windows;                           /* windows registered on this communicator */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,
@@ -151,6 +154,22 @@ ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo);
  * instead of their uncached scratch.  Call only when no all-reduce is in flight on any rank (it
  * overwrites scratch slots). */
 ncclResult_t mncclCommLinkProbe(ncclComm_t comm, int allPeers, size_t bytes, int iters, double* gbps);
+
+/* Registered windows (since 500; NCCL's collective buffer registration).  COLLECTIVE: every rank
+ * calls mncclCommRegister with its buffer of the window -- device memory of its own GPU, the same
+ * `size` on every rank -- in the same order (the window's number is the registration's).  After
+ * it, an ncclAllReduce whose send and recv lie in registered windows -- the SAME windows at the
+ * SAME byte offsets on every rank, with the same count / datatype / op (the symmetric layout of a
+ * data-parallel gradient buffer) -- runs the read schedule with no host rendezvous: the call only
+ * publishes its record and launches, so with MINI_NCCL_BLOCKING=0 a rank returns without waiting
+ * for its peers.  The promise is checked on the device before any peer buffer is touched; a call
+ * that breaks it (other windows or offsets on some rank, or an unregistered buffer where a peer
+ * passed a registered one) fails with ncclInvalidUsage on every rank and the communicator is no
+ * longer usable.  The buffer must stay allocated until mncclCommDeregister (also collective, same
+ * order); calls on buffers outside any window are negotiated per call as before.  *handle
+ * identifies the window; a communicator of one rank accepts and ignores windows. */
+ncclResult_t mncclCommRegister(ncclComm_t comm, void* buff, size_t size, void** handle);
+ncclResult_t mncclCommDeregister(ncclComm_t comm, void* handle);
 
 /* library version, 10000*major + 100*minor + patch */
 int mncclVersion(void);

@@ -193,6 +193,8 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
   }
   snprintf(info->auto_reason, sizeof info->auto_reason, "%s", c->topology_reason().c_str());
   info->read_grid_calls = c->read_grid_calls();
+  info->window_calls = c->window_calls();
+  info->windows = (int)c->windows();
   memcpy(out, &full, size < sizeof full ? size : sizeof full);
   return ncclSuccess;
 }
@@ -219,6 +221,23 @@ ncclResult_t mncclCommLinkProbe(ncclComm_t comm, int allPeers, size_t bytes, int
   } catch (...) {
     return ncclSystemError;
   }
+}
+
+ncclResult_t mncclCommRegister(ncclComm_t comm, void* buff, size_t size, void** handle) {
+  if (!comm || !buff || !handle || size == 0) return ncclInvalidArgument;
+  try {
+    return reinterpret_cast<Comm*>(comm)->register_window(buff, size, handle);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "[Mini-NCCL] CommRegister Error: %s\n", e.what());
+    return ncclInternalError;
+  } catch (...) {
+    return ncclSystemError;
+  }
+}
+
+ncclResult_t mncclCommDeregister(ncclComm_t comm, void* handle) {
+  if (!comm || !handle) return ncclInvalidArgument;
+  return reinterpret_cast<Comm*>(comm)->deregister_window(handle);
 }
 
 int mncclVersion(void) { return MNCCL_VERSION; }

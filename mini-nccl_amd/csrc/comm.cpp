@@ -394,9 +394,15 @@ ncclResult_t Comm::check_status() {
   const uint32_t st = __atomic_load_n(&h_ctl_[0], __ATOMIC_ACQUIRE);
   if (st == 0) return ncclSuccess;
   if (sticky_ == ncclSuccess) {
-    sticky_ = (st & kStatusRemoteAbort) && !(st & kStatusTimeout) ? ncclRemoteError : ncclInternalError;
+    // a registered-window call whose ranks disagreed (kernels.hip starts_agree), seen here or
+    // relayed by the peer that saw it: the caller's error, ncclInvalidUsage
+    const uint64_t a0 = (st & kStatusRemoteAbort) ? reinterpret_cast<const volatile uint64_t*>(h_ctl_ + 4)[3] : 0;
+    const bool mismatch = (st & kStatusMismatch) || ((uint32_t)(a0 >> 32) & kStatusMismatch);
+    sticky_ = mismatch ? ncclInvalidUsage
+              : (st & kStatusRemoteAbort) && !(st & kStatusTimeout) ? ncclRemoteError : ncclInternalError;
     fprintf(stderr, "[Mini-NCCL] rank %d: all-reduce %s (status 0x%x); communicator is no longer usable\n", rank_,
-            (st & kStatusTimeout) ? "timed out (watchdog)" : (st & kStatusHostAbort) ? "aborted by host" : "aborted by a peer",
+            mismatch ? "on registered windows: the ranks passed different windows / offsets / count / datatype / op"
+            : (st & kStatusTimeout) ? "timed out (watchdog)" : (st & kStatusHostAbort) ? "aborted by host" : "aborted by a peer",
             st);
     if ((st & kStatusRemoteAbort) && !(st & (kStatusTimeout | kStatusHostAbort))) {
       // the ABORT word the first aborting peer wrote (kernels.hip abort_word; the host's
@@ -406,6 +412,7 @@ ncclResult_t Comm::check_status() {
       if (a)
         fprintf(stderr, "[Mini-NCCL] rank %d: first abort came from rank %d (%s)\n", rank_, (int)(a & 0xffffffffu) - 1,
                 (why & kStatusTimeout) ? "its watchdog timed out" : (why & kStatusHostAbort) ? "its host aborted"
+                : (why & kStatusMismatch) ? "its peers' call signatures differed from its own"
                 : (why & kStatusRemoteAbort) ? "relaying an abort" : "it gave up outside its kernel");
     }
     if (st & kStatusTimeout) {
@@ -515,7 +522,7 @@ void Comm::wait_previous_call() {
 
 void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
                   uint32_t seq, bool vec, const char* const* psend, const char* const* precv,
-                  size_t tail_bytes) {
+                  size_t tail_bytes, uint64_t sig) {
   const int n = nranks_;
   CollParams p;
   memset(&p, 0, sizeof p);
@@ -556,6 +563,7 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.tail_bytes = tail_bytes;
   p.claim = claim_;
   p.go = go_;
+  p.sig = algo == 2 ? sig : 0;
   const int nt = cfg_.threads, wg = A / geo_.waves;
   // mncclAlgoReadGrid: the push form's large calls as start / grid fold / done (the same on every
   // rank: the schedule, the push form, vec and the size are rank-uniform)
@@ -629,6 +637,46 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     const bool read_sched = !oneshot &&
                             (((algo_ == 2 || algo_ == 4) && (!auto_ || topo_read_)) || (algo_ == 3 && topo_read_)) &&
                             pbuf_.available();
+    // registered windows: the read schedule with no host rendezvous (no record to wait for, no
+    // pointer query) -- every rank promised the same windows and offsets, the kernel checks it
+    const Window* win_s = read_sched && !windows_.empty() ? find_window(send, bytes) : nullptr;
+    const Window* win_r = win_s ? find_window(recv, bytes) : nullptr;
+    if (win_s && win_r) {
+      const uint64_t os = (uint64_t)((const char*)send - win_s->base), orv = (uint64_t)((char*)recv - win_r->base);
+      const char* psend[kMaxRanks] = {};
+      const char* precv[kMaxRanks] = {};
+      for (int q = 0; q < n; ++q) {
+        psend[q] = win_s->peer[q] + os;
+        precv[q] = win_r->peer[q] + orv;
+      }
+      // the call's signature: windows, offsets, count, datatype, op (FNV-1a over the words)
+      uint64_t sig = 1469598103934665603ull;
+      for (uint64_t v : {win_s->id, os, win_r->id, orv, (uint64_t)count, (uint64_t)dtype, (uint64_t)op, (uint64_t)algo_})
+        for (int b = 0; b < 8; ++b) sig = (sig ^ ((v >> (8 * b)) & 0xff)) * 1099511628211ull;
+      sig |= 1;  // never 0 (0 = a negotiated call)
+      try {
+        pbuf_.publish_fast(count, dtype, op, sig, cfg_.timeout_ms / 1000.0 + 2.0);
+      } catch (const PeerGaveUp& e) {
+        return rendezvous_failed(e, true, cur_dev);
+      } catch (const std::exception& e) {
+        return rendezvous_failed(e, false, cur_dev);
+      }
+      const bool vec_w = win_s->aligned && win_r->aligned && os % 4 == 0 && orv % 4 == 0 && chunk_bytes % 4 == 0;
+      const size_t body = chunk_bytes * (size_t)n;
+      const size_t tail = send != recv && bytes > body ? bytes - body : 0;
+      seq = ++call_seq_;
+      if (seq == 0) seq = ++call_seq_;
+      launch(2, send, recv, chunk_bytes, dtype, op, stream, seq, vec_w, psend, precv, tail, sig);
+      ++window_calls_;
+      if (!capturing) {
+        hip_check(hipEventRecord(order_ev_, stream), "order event");
+        last_stream_ = stream;
+        have_last_ = true;
+      }
+      if (cur_dev != device_) hipSetDevice(cur_dev);
+      if (cfg_.blocking && !capturing) return wait_for(stream, seq);
+      return ncclSuccess;
+    }
     if (read_sched) pbuf_.reap(send, recv);
     const Reach rs = read_sched && pbuf_.known(send) ? (local_s = true, Reach::kDevice) : reach(send, &ksend, &local_s);
     const Reach rr = read_sched && pbuf_.known(recv) ? (local_r = true, Reach::kDevice)
@@ -671,15 +719,16 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
         d = pbuf_.negotiate(send, recv, eligible, count, dtype, op, cfg_.timeout_ms / 1000.0 + 2.0,
                             [this] { wait_previous_call(); }, psend, precv, &vec_all);
       } catch (const PeerGaveUp& e) {
-        // a peer's communicator died in an earlier rendezvous: as a peer's ABORT in the kernel
-        fprintf(stderr, "[Mini-NCCL] rank %d: %s; communicator is no longer usable\n", rank_, e.what());
-        sticky_ = ncclRemoteError;
-        if (cur_dev != device_) hipSetDevice(cur_dev);
-        return sticky_;
+        return rendezvous_failed(e, true, cur_dev);
       } catch (const std::exception& e) {
-        fprintf(stderr, "[Mini-NCCL] rank %d: %s; communicator is no longer usable\n", rank_, e.what());
-        sticky_ = ncclInternalError;
-        abort_peers();
+        return rendezvous_failed(e, false, cur_dev);
+      }
+      if (d == PeerBuffers::kWindowPeer) {
+        fprintf(stderr, "[Mini-NCCL] rank %d: a peer ran this all-reduce on registered windows, this rank's buffers "
+                "are not in them (every rank must pass buffers of the same windows); communicator is no longer "
+                "usable\n", rank_);
+        sticky_ = ncclInvalidUsage;
+        abort_peers();  // the peer's kernel waits for this rank's START: fail it now
         if (cur_dev != device_) hipSetDevice(cur_dev);
         return sticky_;
       }
@@ -708,6 +757,108 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
   if (cur_dev != device_) hipSetDevice(cur_dev);
   if (cfg_.blocking && cap == hipStreamCaptureStatusNone) return wait_for(stream, seq);
   return ncclSuccess;
+}
+
+ncclResult_t Comm::rendezvous_failed(const std::exception& e, bool peer_gave_up, int cur_dev) {
+  fprintf(stderr, "[Mini-NCCL] rank %d: %s; communicator is no longer usable\n", rank_, e.what());
+  if (peer_gave_up) {
+    // a peer's communicator died in an earlier rendezvous: as a peer's ABORT in the kernel
+    sticky_ = ncclRemoteError;
+  } else {
+    sticky_ = ncclInternalError;
+    abort_peers();
+  }
+  if (cur_dev != device_) hipSetDevice(cur_dev);
+  return sticky_;
+}
+
+const Comm::Window* Comm::find_window(const void* p, size_t bytes) const {
+  const char* c = static_cast<const char*>(p);
+  for (const Window& w : windows_)
+    if (c >= w.base && (size_t)(c - w.base) <= w.bytes && bytes <= w.bytes - (size_t)(c - w.base)) return &w;
+  return nullptr;
+}
+
+// Collective: every rank registers its buffer of the window (same size) in the same order.  One
+// negotiated rendezvous of the read schedule maps every rank's buffer here (the same dma-buf
+// imports the negotiated calls use, kept until the owner frees the allocation); the window's
+// number is the registration's, the same on every rank.
+ncclResult_t Comm::register_window(void* buf, size_t bytes, void** handle) {
+  *handle = nullptr;
+  if (sticky_ != ncclSuccess) return sticky_;
+  if (check_status() != ncclSuccess) return sticky_;
+  if (!buf || bytes == 0) return ncclInvalidArgument;
+  int cur_dev = -1;
+  hip_check(hipGetDevice(&cur_dev), "hipGetDevice");
+  if (cur_dev != device_) hip_check(hipSetDevice(device_), "hipSetDevice");
+  Window w;
+  memset(&w, 0, sizeof w);
+  w.base = static_cast<const char*>(buf);
+  w.bytes = bytes;
+  if (nranks_ == 1) {
+    w.id = next_window_++;
+    w.peer[0] = w.base;
+    w.aligned = (uintptr_t)buf % 4 == 0;
+    windows_.push_back(w);
+    *handle = (void*)(uintptr_t)w.id;
+    if (cur_dev != device_) hipSetDevice(cur_dev);
+    return ncclSuccess;
+  }
+  if (!pbuf_.available()) {
+    fprintf(stderr, "[Mini-NCCL] rank %d: registered windows need the read schedule's shared board, which is off\n",
+            rank_);
+    if (cur_dev != device_) hipSetDevice(cur_dev);
+    return ncclInvalidUsage;  // the board is off on every rank alike: every rank returns this
+  }
+  pbuf_.reap(buf, buf);
+  bool local = false;
+  const void* kp = buf;
+  const bool eligible = pbuf_.known(buf) || (reach(buf, &kp, &local) == Reach::kDevice && local);
+  const char* psend[kMaxRanks] = {};
+  const char* precv[kMaxRanks] = {};
+  bool vec_all = false;
+  PeerBuffers::Decision d = PeerBuffers::kFallback;
+  constexpr int kRegisterDtype = 0x52;  // never an all-reduce's: a call cannot pair with a registration
+  try {
+    d = pbuf_.negotiate(buf, buf, eligible, bytes, kRegisterDtype, 0, cfg_.timeout_ms / 1000.0 + 2.0,
+                        [this] { wait_previous_call(); }, psend, precv, &vec_all);
+  } catch (const PeerGaveUp& e) {
+    return rendezvous_failed(e, true, cur_dev);
+  } catch (const std::exception& e) {
+    return rendezvous_failed(e, false, cur_dev);
+  }
+  if (cur_dev != device_) hipSetDevice(cur_dev);
+  if (d == PeerBuffers::kWindowPeer) {
+    sticky_ = ncclInvalidUsage;
+    abort_peers();
+    return sticky_;
+  }
+  if (d == PeerBuffers::kMismatch) {
+    fprintf(stderr, "[Mini-NCCL] rank %d: mncclCommRegister: the ranks registered windows of different sizes (or a "
+            "rank called an all-reduce instead)\n", rank_);
+    return ncclInvalidUsage;
+  }
+  if (d != PeerBuffers::kRead) {
+    fprintf(stderr, "[Mini-NCCL] rank %d: mncclCommRegister: some rank's buffer is not device memory of its GPU "
+            "that the peers can map\n", rank_);
+    return ncclInvalidUsage;
+  }
+  w.id = next_window_++;
+  for (int q = 0; q < nranks_; ++q) w.peer[q] = psend[q];
+  w.aligned = vec_all;
+  windows_.push_back(w);
+  *handle = (void*)(uintptr_t)w.id;
+  return ncclSuccess;
+}
+
+ncclResult_t Comm::deregister_window(void* handle) {
+  const uint64_t id = (uint64_t)(uintptr_t)handle;
+  for (size_t i = 0; i < windows_.size(); ++i)
+    if (windows_[i].id == id) {
+      windows_.erase(windows_.begin() + (long)i);
+      return ncclSuccess;
+    }
+  return ncclInvalidArgument;
 }
 
 void Comm::abort_peers() {

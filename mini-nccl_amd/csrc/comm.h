@@ -5,6 +5,7 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -41,6 +42,13 @@ class Comm {
     algo_ = a < 0 ? 2 : a;
   }
   int last_algo() const { return last_algo_; }  // schedule of the last launched kernel, -1: none
+  // Registered windows (mncclCommRegister / mncclCommDeregister, collective): a call whose send and
+  // recv lie in windows -- the same windows at the same offsets on every rank -- runs the read
+  // schedule with no host rendezvous (kernels.hip starts_agree checks the promise on the device)
+  ncclResult_t register_window(void* buf, size_t bytes, void** handle);
+  ncclResult_t deregister_window(void* handle);
+  size_t windows() const { return windows_.size(); }
+  unsigned long long window_calls() const { return window_calls_; }
   unsigned long long read_grid_calls() const { return read_grid_calls_; }  // calls run in the grid form
   size_t peer_mappings() const { return pbuf_.mapped_allocations(); }
   const PeerBuffers& peer_buffers() const { return pbuf_; }
@@ -76,7 +84,17 @@ class Comm {
   // algo: 0 ring, 2 read (psend / precv: every rank's buffers mapped here), 3 one-shot
   void launch(int algo, const void* send, void* recv, size_t chunk_bytes, int dtype, int op, hipStream_t stream,
               uint32_t seq, bool vec, const char* const* psend = nullptr, const char* const* precv = nullptr,
-              size_t tail_bytes = 0);
+              size_t tail_bytes = 0, uint64_t sig = 0);
+  // one rendezvous failure of the read schedule, reported like the kernel's (sticky, peers aborted)
+  ncclResult_t rendezvous_failed(const std::exception& e, bool peer_gave_up, int cur_dev);
+  struct Window {
+    uint64_t id;                    // registration number, the same on every rank
+    const char* base;               // this rank's buffer
+    size_t bytes;
+    const char* peer[kMaxRanks];    // every rank's buffer of this window, mapped here
+    bool aligned;                   // every rank's base is dword-aligned
+  };
+  const Window* find_window(const void* p, size_t bytes) const;
   void wait_previous_call();
   ncclResult_t check_status();
   // a rank that gives up on a call outside its kernel (the read schedule's rendezvous) raises
@@ -92,6 +110,9 @@ class Comm {
   bool auto_ = true;             // the default: as algo_ = 2, with the ring's small calls one-shot
   int last_algo_ = -1;
   unsigned long long read_grid_calls_ = 0;  // read calls launched as start / grid / done
+  std::vector<Window> windows_;
+  uint64_t next_window_ = 1;
+  unsigned long long window_calls_ = 0;     // calls launched on registered windows (no rendezvous)
   int ranks_on_device_ = 1;
   bool topo_read_ = true;        // auto may run the read schedule (every pair: same GPU or 1 xGMI hop)
   std::string topo_why_ = "read: one rank";

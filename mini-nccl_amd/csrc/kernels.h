@@ -42,6 +42,9 @@ struct CollParams {
                               // only that lane writes the status and its diagnostic
   uint32_t* go;               // device word: the read schedule's grid form -- call_seq once START
                               // is through (read_start_kernel), checked by the grid and DONE launches
+  uint64_t sig;               // registered-window call (no host rendezvous): this call's signature,
+                              // sent with START and compared with every peer's before any peer
+                              // buffer is touched (0: a negotiated call, nothing to check)
 };
 
 constexpr int kMaxRanks = 16;

@@ -301,6 +301,43 @@ __device__ __forceinline__ bool wave_wait_peers(const u64* flag, u64 target, boo
   return __builtin_amdgcn_ballot_w64(bad != 0) == 0;
 }
 
+// Registered-window calls (Comm::allreduce's fast path) are launched without a host rendezvous: the
+// peers' buffer addresses come from the windows every rank registered together, on the promise
+// that every rank passes the same windows, offsets, count, dtype and op.  The promise is checked
+// here, on the device, before any peer buffer is touched: START carries the caller's signature
+// (a hash of those) in word kSigWord of the READY line, stored and drained before the flag; after
+// every peer's START, lane q compares peer q's signature with this rank's and clears the word (a
+// later call can never match a stale one).  Any difference -- seen by every rank alike, as every
+// rank compares every pair it is part of -- gives up the call with kStatusMismatch (ncclInvalidUsage).
+// The START of read_start_kernel; read_kernel writes the same stores inline, its flag value read
+// inside the peer-lane branch (read outside it, from a clamped LDS index, the persistent kernel's
+// fold spilled 36 registers to scratch at the 256-register bound).
+__device__ __forceinline__ void send_start(const CollParams& p, int C, int lane, u64 v, int w) {
+  const int n = p.n, r = p.rank;
+  if (lane < n && lane != r && p.sig) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w) + kSigWord, p.sig);
+  if (p.sig) drain_stores();  // the signature has landed before the flag can be seen
+  if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), v);
+}
+
+// lane q: does peer q's signature differ from mine?  Clears the word.  Out of line: kept out of
+// the persistent kernel's register allocation, whose fold sits at the 256-register bound
+__device__ __noinline__ bool sig_differs(u64* word, u64 sig) {
+  const bool bad = ld_sys(word) != sig;
+  st_sys(word, 0);
+  return bad;
+}
+
+// after every peer's START: false (status claimed, nothing touched) if some peer's signature differs
+__device__ __forceinline__ bool starts_agree(const CollParams& p, const Ctl& c, int C, int lane, int w) {
+  if (!p.sig) return true;
+  const int n = p.n, r = p.rank;
+  bool bad = false;
+  if (lane < n && lane != r) bad = sig_differs(p.mbox + mbox_ready(C, lane, w) + kSigWord, p.sig);
+  if (__builtin_amdgcn_ballot_w64(bad) == 0) return true;
+  if (lane == 0 && claim_first(c)) st_sys32(c.status, kStatusMismatch);
+  return false;
+}
+
 // ---------------------------------------------------------------- message bodies (one wave)
 enum : int { kHasLocal = 1, kHasIn = 2, kWritesRecv = 4, kSends = 8, kReduces = 16 };
 template <int KIND> struct KindBits;
@@ -805,11 +842,16 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
     rx[lane] = p.rx_seq[(u64)lane * C + w];
   }
   __builtin_amdgcn_wave_barrier();
-  // START to every peer, then wait for theirs
+  // START to every peer (with the call's signature on a registered-window call), then wait for theirs
+  if (lane < n && lane != r) {
+    if (p.sig) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w) + kSigWord, p.sig);
+  }
+  if (p.sig) drain_stores();  // the signature has landed before the flag can be seen
   if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + 1);
   if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), rx[lane < n ? lane : 0] + 1, lane < n && lane != r, ctl, lane,
                        true))
     goto aborted;
+  if (!starts_agree(p, ctl, C, lane, w)) goto aborted;
   acquire_sys(p.sys_fence);
   for (uint32_t j = 0; j <= iters; ++j) {
     if (j < iters) {
@@ -910,8 +952,9 @@ __global__ void __launch_bounds__(64) read_start_kernel(CollParams p) {
   const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox, p.claim};
   const bool peer = lane < n && lane != r;
   const u64 tx = peer ? p.tx_seq[(u64)lane * C] : 0, rx = peer ? p.rx_seq[(u64)lane * C] : 0;
-  if (peer) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, 0), tx + 1);
-  const bool ok = wave_wait_peers(p.mbox + mbox_ready(C, lane, 0), rx + 1, peer, ctl, lane, true);
+  send_start(p, C, lane, tx + 1, 0);
+  const bool ok = wave_wait_peers(p.mbox + mbox_ready(C, lane, 0), rx + 1, peer, ctl, lane, true) &&
+                  starts_agree(p, ctl, C, lane, 0);
   // 0 after a failed START (a graph replay reuses call_seq: the word must not keep a stale "go")
   if (lane == 0) *p.go = ok ? p.call_seq : 0u;
   if (!ok && lane == 0)

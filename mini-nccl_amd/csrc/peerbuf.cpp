@@ -56,6 +56,10 @@ struct alignas(64) CallRec {
   BufDesc send, recv;
   int32_t nfreed;
   uint64_t freed[kMaxFreed][2];  // (base, id) of this rank's exported allocations freed since its last record
+  // a registered-window call (publish_fast): this rank did not wait for the others' records, its
+  // kernel checks the call's signature on the device
+  int32_t fast;
+  uint64_t sig;
   // second round (only when some rank may have to open a new mapping): the call whose mapping
   // outcome map_ok reports, stored after it (release)
   alignas(64) std::atomic<uint64_t> mapped;
@@ -329,6 +333,47 @@ char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, int fd, const ipc
   return p;
 }
 
+void PeerBuffers::publish_fast(uint64_t count, int dtype, int op, uint64_t sig, double timeout_s) {
+  const uint64_t k = ++seq_;
+  const double t0 = now_s();
+  const int slot = (int)(k % kBoardDepth);
+  try {
+    // my record slot is free once every peer has read the record kBoardDepth calls back (a peer on
+    // registered windows too marks its records read as it publishes them): a rank runs at most
+    // kBoardDepth calls ahead of its slowest peer, the only host-side wait of a window call
+    if (k > (uint64_t)kBoardDepth)
+      for (int q = 0; q < nranks_; ++q) {
+        if (q == rank_) continue;
+        for (int spins = 0; board_->consumed[q].v.load(std::memory_order_acquire) < k - kBoardDepth; ++spins) {
+          if (board_->gave_up[q].v.load(std::memory_order_acquire) != 0)
+            throw PeerGaveUp("read schedule: rank " + std::to_string(q) + " abandoned the communicator before all-reduce #" +
+                             std::to_string(k));
+          if (now_s() - t0 > timeout_s)
+            throw std::runtime_error("registered windows: rank " + std::to_string(q) + " stayed more than " +
+                                     std::to_string(kBoardDepth) + " calls behind for " + std::to_string((int)timeout_s) +
+                                     " s (all-reduce #" + std::to_string(k) + ")");
+          backoff(spins);
+        }
+      }
+  } catch (...) {
+    board_->gave_up[rank_].v.store(k, std::memory_order_release);
+    throw;
+  }
+  CallRec& me = board_->rec[rank_][slot];
+  me.count = count;
+  me.dtype = dtype;
+  me.op = op;
+  me.eligible = 1;
+  me.aligned = 1;
+  memset(&me.send, 0, sizeof me.send);
+  memset(&me.recv, 0, sizeof me.recv);
+  me.nfreed = 0;  // frees wait for this rank's next negotiated record
+  me.fast = 1;
+  me.sig = sig;
+  me.seq.store(k, std::memory_order_release);
+  board_->consumed[rank_].v.store(k, std::memory_order_release);  // nothing of this call to read
+}
+
 PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv, bool eligible, uint64_t count,
                                              int dtype, int op, double timeout_s,
                                              const std::function<void()>& sync_previous, const char** psend,
@@ -499,6 +544,8 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
   me.count = count;
   me.dtype = dtype;
   me.op = op;
+  me.fast = 0;
+  me.sig = 0;
   me.eligible = ok ? 1 : 0;
   me.aligned = ((sd.raw | rd.raw) % 4 == 0) ? 1 : 0;
   me.send = sd;
@@ -514,7 +561,7 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
 
   struct Seen {
     uint64_t count;
-    int32_t dtype, op, eligible, aligned;
+    int32_t dtype, op, eligible, aligned, fast;
     BufDesc send, recv;
     int32_t nfreed;
     uint64_t freed[kMaxFreed][2];
@@ -529,12 +576,18 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
     s.op = c.op;
     s.eligible = c.eligible;
     s.aligned = c.aligned;
+    s.fast = c.fast;
     s.send = c.send;
     s.recv = c.recv;
     s.nfreed = c.nfreed < 0 ? 0 : c.nfreed > kMaxFreed ? kMaxFreed : c.nfreed;
     memcpy(s.freed, c.freed, sizeof s.freed);
   }
   board_->consumed[rank_].v.store(k, std::memory_order_release);  // my copies are taken
+  // a peer launched this call on its registered windows without waiting for the records: it takes
+  // for granted that every rank does, and this rank's buffers are not in them -- the caller broke
+  // the windows' contract (Comm fails the call on every rank, the peer's kernel through its ABORT)
+  for (const Seen& c : recs)
+    if (c.fast) return kWindowPeer;
 
   // the peers' freed allocations: forget them (every rank alike) and close my imports of them.
   // The owner's call that used one last ended only after every peer's kernel was done with it

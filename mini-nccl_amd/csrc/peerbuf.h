@@ -54,7 +54,9 @@ class PeerBuffers {
   void init(Bootstrap& boot, int rank, int nranks, const std::vector<uint64_t>& nonces, int port);
   bool available() const { return board_ != nullptr; }
 
-  enum Decision { kRead = 1, kFallback = 0, kMismatch = -1 };
+  // kWindowPeer: a peer ran this call on registered windows (publish_fast) while this rank's
+  // buffers are not in them -- the caller broke the windows' contract
+  enum Decision { kRead = 1, kFallback = 0, kMismatch = -1, kWindowPeer = -2 };
   // One call's rendezvous.  `eligible`: this rank's buffers are device memory (the rendezvous
   // also requires them to be memory of this rank's GPU, and shareable).  On kRead, psend /
   // precv[q] hold rank q's buffers mapped here (this rank's own at [rank]) and *vec_all whether
@@ -64,6 +66,12 @@ class PeerBuffers {
   Decision negotiate(const void* send, const void* recv, bool eligible, uint64_t count, int dtype, int op,
                      double timeout_s, const std::function<void()>& sync_previous, const char** psend,
                      const char** precv, bool* vec_all);
+
+  // A registered-window call (Comm::allreduce's fast path): this rank's record for the next call,
+  // marked fast with the call's signature, published WITHOUT reading the peers' -- their kernels
+  // check the signature on the device (kernels.hip starts_agree).  Waits only while the record
+  // slot is still unread by some peer (kBoardDepth calls behind); throws as negotiate does.
+  void publish_fast(uint64_t count, int dtype, int op, uint64_t sig, double timeout_s);
 
   // This rank's exported allocations freed since the last call are found and queued for its next
   // record: every export holding send or recv is checked (so known() below cannot name a freed

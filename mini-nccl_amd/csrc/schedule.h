@@ -277,6 +277,13 @@ MNCCL_HD int topology_blocks_read(int n, const int* link, const int* hops) {
 }
 
 // Kernel status bits (host-mapped status word)
-enum : uint32_t { kStatusTimeout = 1u, kStatusHostAbort = 2u, kStatusRemoteAbort = 4u };
+// kStatusMismatch: a registered-window call whose ranks passed different windows / offsets / count /
+// dtype / op (the START signatures differ, read_kernel): no data was touched, the call fails with
+// ncclInvalidUsage on every rank.
+enum : uint32_t { kStatusTimeout = 1u, kStatusHostAbort = 2u, kStatusRemoteAbort = 4u, kStatusMismatch = 8u };
+
+// Word of a READY line (mbox_ready, 16 words per line) that carries the sender's call signature
+// with its START of a registered-window call (0 = none).
+constexpr int kSigWord = 1;
 
 }  // namespace mnccl

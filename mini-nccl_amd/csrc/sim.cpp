@@ -38,6 +38,8 @@ struct World {
   std::vector<std::vector<char>> scratch;     // per rank
   std::vector<std::vector<uint64_t>> mbox;    // per rank
   std::vector<std::vector<uint64_t>> tx_seq, rx_seq;  // per rank: [peer * C + w]
+  std::vector<uint64_t> sig;           // registered-window call: each rank's START signature (empty: none)
+  std::vector<int> mismatch;           // per rank: pipelines that saw a differing signature
 
   // message `seq` from src to dst on pipeline w (schedule.h msg_slot_off: the receiver's scratch)
   char* slot(int src, int dst, int w, uint64_t seq) {
@@ -139,12 +141,28 @@ bool read_step(World& W, Prog& P) {
   };
   switch (P.j) {
     case 0:
+      // START (kernels.hip read_kernel): a registered-window call's signature lands first
+      if (!W.sig.empty())
+        for (int k = 1; k < n; ++k) W.mbox[direct_peer(n, r, k)][mbox_ready(W.C, r, w) + kSigWord] = W.sig[r];
       for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx(direct_peer(n, r, k)) + 1;
       P.j = 1;
       return true;
     case 1:
       for (int k = 1; k < n; ++k)
         if (W.ready(r, direct_peer(n, r, k), w) < rx(direct_peer(n, r, k)) + 1) return false;
+      if (!W.sig.empty()) {  // kernels.hip starts_agree: compare, clear, give up before any data
+        bool bad = false;
+        for (int k = 1; k < n; ++k) {
+          uint64_t& word = W.mbox[r][mbox_ready(W.C, direct_peer(n, r, k), w) + kSigWord];
+          bad = bad || word != W.sig[r];
+          word = 0;
+        }
+        if (bad) {
+          ++W.mismatch[r];
+          P.done = true;
+          return true;
+        }
+      }
       P.j = 2;
       P.it = 0;
       P.k = 0;
@@ -378,6 +396,63 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
   }
   if (steps_out) *steps_out = steps;
   return 0;
+}
+
+// One read call (push form) on registered windows: every rank's START carries sigs[r] and every
+// pipeline compares its peers' with its own before touching data (kernels.hip starts_agree).
+// mismatch_out[r] = pipelines of rank r that gave up.  0: every pipeline ran; 1: some gave up
+// (then every pipeline must have, and no recv touched); -1 deadlock; -2 bad arguments.
+int mnccl_sim_signed_read(const float* const* send, float* const* recv, int n, uint64_t count, int channels,
+                          uint64_t slice_bytes, const uint64_t* sigs, uint64_t schedule_seed, int* mismatch_out) {
+  if (n < 2 || n > 16 || channels < 1 || slice_bytes < 4 || slice_bytes % 4) return -2;
+  World W;
+  W.n = n; W.C = channels; W.K = 2; W.op = 0; W.algo = 2; W.slot_bytes = slice_bytes; W.push = true;
+  W.chunk_bytes = count / (uint64_t)n * 4;
+  W.send.assign(send, send + n);
+  W.recv.assign(recv, recv + n);
+  W.mbox.assign((size_t)n, std::vector<uint64_t>((size_t)mbox_words(n, channels), 0));
+  W.tx_seq.assign((size_t)n, std::vector<uint64_t>((size_t)n * channels, 0));
+  W.rx_seq.assign((size_t)n, std::vector<uint64_t>((size_t)n * channels, 0));
+  W.sig.assign(sigs, sigs + n);
+  W.mismatch.assign((size_t)n, 0);
+  W.slice = slice_bytes;
+  W.nslices = (W.chunk_bytes + W.slice - 1) / W.slice;
+  W.A = call_pipelines(W.nslices, channels, 1);
+  W.iters = (uint32_t)((W.nslices + (uint64_t)W.A - 1) / (uint64_t)W.A);
+  if (W.chunk_bytes == 0) return -2;
+  std::vector<Prog> progs;
+  for (int r = 0; r < n; ++r)
+    for (int w = 0; w < W.A; ++w) {
+      Prog p;
+      p.r = r; p.w = w;
+      progs.push_back(p);
+    }
+  uint64_t rng = schedule_seed * 6364136223846793005ull + 1442695040888963407ull;
+  for (;;) {
+    bool any = false, all_done = true;
+    const size_t np = progs.size();
+    rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+    const size_t start = (size_t)((rng >> 33) % np);
+    for (size_t j = 0; j < np; ++j) {
+      Prog& P = progs[(start + j) % np];
+      if (P.done) continue;
+      all_done = false;
+      rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+      const int burst = 1 + (int)((rng >> 40) % 4);
+      for (int b = 0; b < burst && !P.done; ++b) {
+        if (!read_step(W, P)) break;
+        any = true;
+      }
+    }
+    if (all_done) break;
+    if (!any) return -1;
+  }
+  int total = 0;
+  for (int r = 0; r < n; ++r) {
+    mismatch_out[r] = W.mismatch[r];
+    total += W.mismatch[r];
+  }
+  return total ? 1 : 0;
 }
 
 }  // extern "C"

@@ -59,6 +59,7 @@ class CommInfo(ctypes.Structure):
         # since mncclVersion 500
         ("auto_read", ctypes.c_int), ("peer_link", ctypes.c_int * 16), ("peer_hops", ctypes.c_int * 16),
         ("auto_reason", ctypes.c_char * 160), ("read_grid_calls", ctypes.c_ulonglong),
+        ("window_calls", ctypes.c_ulonglong), ("windows", ctypes.c_int),
     ]
 
 
@@ -77,6 +78,8 @@ SIGNATURES = {
     "mncclCommGetInfoV": (_I, [_VP, _VP, _SZ]),
     "mncclCommSetAlgo": (_I, [_VP, _I]),
     "mncclCommLinkProbe": (_I, [_VP, _I, _SZ, _I, ctypes.POINTER(ctypes.c_double)]),
+    "mncclCommRegister": (_I, [_VP, _VP, _SZ, ctypes.POINTER(_VP)]),
+    "mncclCommDeregister": (_I, [_VP, _VP]),
     "mncclVersion": (_I, []),
 }
 
@@ -161,6 +164,20 @@ class Comm:
         mode = int(bool(all_peers)) | (self.PROBE_FORMS[form] << 1) | (8 if pull else 0) | (16 if user else 0)
         check(load().mncclCommLinkProbe(self.handle, mode, nbytes, iters, ctypes.byref(g)), "mncclCommLinkProbe")
         return g.value
+
+    def register(self, ptr, nbytes):
+        """mncclCommRegister (collective): returns the window handle."""
+        h = ctypes.c_void_p()
+        check(load().mncclCommRegister(self.handle, ptr, nbytes, ctypes.byref(h)), "mncclCommRegister")
+        return h
+
+    def register_rc(self, ptr, nbytes):
+        """mncclCommRegister's result code (does not raise) and the handle."""
+        h = ctypes.c_void_p()
+        return load().mncclCommRegister(self.handle, ptr, nbytes, ctypes.byref(h)), h
+
+    def deregister(self, h):
+        return check(load().mncclCommDeregister(self.handle, h), "mncclCommDeregister")
 
     def set_algo(self, algo):
         return check(load().mncclCommSetAlgo(self.handle, algo))

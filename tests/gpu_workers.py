@@ -821,6 +821,113 @@ def cached_consumer_rank(rank, n, port, env, count, calls, out_q, barrier=None):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def window_rank(rank, n, port, env, scenario, out_q, barrier=None):
+    """Registered windows (mncclCommRegister): calls whose send / recv lie in the windows at the same
+    offsets on every rank run the read schedule with no host rendezvous.
+      parity   -- calls on sub-ranges of two windows (and in place in one), several sizes / dtypes /
+                  ops, varying data, interleaved with negotiated and ring calls: bit-exact, and
+                  window_calls counts exactly the window calls
+      async    -- MINI_NCCL_BLOCKING=0, rank 1 sleeps 50 ms before each call: rank 0's call returns
+                  without waiting for it (host time reported), results bit-exact
+      mismatch -- rank 0 passes another offset: every rank's call fails with ncclInvalidUsage
+      unregistered -- rank 0 passes window buffers, the others buffers outside any window: every
+                  rank fails fast (no watchdog wait)"""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        use_rank_device(rank)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        st = hip_rt.Stream()
+        wbytes = 16 << 20
+        sbuf, rbuf = hip_rt.DeviceBuffer(wbytes, fresh=True), hip_rt.DeviceBuffer(wbytes, fresh=True)
+        hs = comm.register(sbuf.ptr, wbytes)
+        hr = comm.register(rbuf.ptr, wbytes)
+        res = {"windows": comm.info()["windows"]}
+        if scenario == "parity":
+            # (dtype, op, count, send offset, recv offset or None = in place in the send window, algo)
+            plan = [("f32", "sum", (1 << 20) + 5, 0, 0, -1), ("bf16", "sum", 300007, 4096, 8192, -1),
+                    ("f32", "max", 77777, 1 << 20, None, -1), ("f64", "prod", 4099, 64, 128, 2),
+                    ("f32", "sum", 1000, 256, 512, -1), ("i32", "min", n * 1024, 1 << 22, 1 << 22, 2),
+                    ("f16", "sum", 9 * 4096 + 3, 12, 36, -1), ("f32", "sum", (2 << 20) + 1, 0, None, 4)]
+            bad, rcs, kinds, wc = [], [], [], []
+            for i, (dt, op, count, so, ro, algo) in enumerate(plan * 2):
+                comm.set_algo(algo)
+                code, npd = O.DTYPES[dt]
+                inplace = ro is None
+                xs = make_inputs(n, count, dt, 3000 + i, op in ("max", "min"))
+                exp = O.allreduce(xs, dt, op, inplace=inplace)[rank]
+                sp, rp = sbuf.ptr + so, sbuf.ptr + so if inplace else rbuf.ptr + ro
+                sbuf.upload(xs[rank], so)
+                hip_rt.sync()
+                barrier.wait(120)
+                w0 = comm.info()["window_calls"]
+                rcs.append(comm.all_reduce(sp, rp, count, code, O.OPS[op], st.handle))
+                st.sync()
+                got = (sbuf if inplace else rbuf).download(npd, count, so if inplace else ro)
+                bad.append(compare(got, exp, dt, op in ("sum", "prod"))[0])
+                ci = comm.info()
+                kinds.append(ci["last_algo"])
+                wc.append(ci["window_calls"] - w0)
+                if i % 3 == 2:  # a negotiated call (buffers outside the windows) and a ring call between
+                    other = hip_rt.DeviceBuffer(4 * 5003)
+                    ys = make_inputs(n, 5003, "f32", 3500 + i, False)
+                    other.upload(ys[rank])
+                    hip_rt.sync()
+                    barrier.wait(120)
+                    comm.set_algo(-1 if i % 2 else 0)
+                    rcs.append(comm.all_reduce(other.ptr, other.ptr, 5003, M.ncclFloat, M.ncclSum, st.handle))
+                    st.sync()
+                    bad.append(compare(other.download(np.float32, 5003), O.allreduce(ys, inplace=True)[rank], "f32",
+                                       True)[0])
+                    other.free()
+            res.update(bad=bad, rcs=rcs, kinds=kinds, wc=wc)
+        elif scenario == "async":
+            count = (1 << 20) + 3
+            times, bad = [], []
+            for c in range(4):
+                xs = make_inputs(n, count, "f32", 3700 + c, False)
+                sbuf.upload(xs[rank])
+                hip_rt.sync()
+                barrier.wait(120)
+                if rank == 1:
+                    time.sleep(0.05)
+                t0 = time.perf_counter()
+                rc = comm.all_reduce(sbuf.ptr, rbuf.ptr, count, M.ncclFloat, M.ncclSum, st.handle)
+                times.append(time.perf_counter() - t0)
+                st.sync()
+                bad.append(-1 if rc else compare(rbuf.download(np.float32, count), O.allreduce(xs)[rank], "f32", True)[0])
+            res.update(call_s=times, bad=bad, window_calls=comm.info()["window_calls"])
+        elif scenario in ("mismatch", "unregistered"):
+            count = 100003
+            other = hip_rt.DeviceBuffer(count * 4)
+            barrier.wait(120)
+            t0 = time.time()
+            if scenario == "mismatch":
+                off = 4096 if rank == 0 else 0
+                rc = comm.all_reduce(sbuf.ptr + off, rbuf.ptr + off, count, M.ncclFloat, M.ncclSum, st.handle)
+            else:
+                p = sbuf.ptr if rank == 0 else other.ptr
+                rc = comm.all_reduce(p, p, count, M.ncclFloat, M.ncclSum, st.handle)
+            res.update(rc=rc, secs=time.time() - t0, async_=comm.async_error(),
+                       rc2=comm.all_reduce(sbuf.ptr, rbuf.ptr, count, M.ncclFloat, M.ncclSum, st.handle))
+            other.free()
+        res["info"] = comm.info()
+        if scenario in ("parity", "async"):
+            comm.deregister(hs)
+            comm.deregister(hr)
+            res["windows_after"] = comm.info()["windows"]
+        st.destroy()
+        res["destroy"] = comm.destroy()
+        sbuf.free()
+        rbuf.free()
+        out_q.put((rank, res))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
 def device_count_probe(out_q):
     import hip_rt
     out_q.put((0, {"count": hip_rt.device_count()}))

@@ -25,6 +25,8 @@ def load():
         L.mnccl_read_slice.restype = u64
         L.mnccl_call_pipelines.argtypes = [u64, i, i]
         L.mnccl_topology_blocks_read.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.mnccl_sim_signed_read.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64,
+                                            ctypes.POINTER(u64), u64, ctypes.POINTER(i)]
         L.mnccl_oneshot_slice.argtypes = [u64, i, i, u64]
         L.mnccl_oneshot_slice.restype = u64
         L.mnccl_oneshot_fits.argtypes = [u64, i, i, u64, i]
@@ -122,3 +124,22 @@ def topology_blocks_read(link, hops):
     flat_h = (ctypes.c_int * (n * n))(*[hops[q][p] for q in range(n) for p in range(n)])
     bad = load().mnccl_topology_blocks_read(n, flat_l, flat_h)
     return None if bad == 0 else divmod(bad - 1, n)
+
+
+def signed_read(inputs, sigs, slice_bytes=1024, channels=4, seed=1):
+    """One read call (push form) on registered windows through the simulated kernels: rank r's
+    START carries sigs[r], every pipeline checks its peers' before touching data (kernels.hip
+    starts_agree).  Returns (recv buffers, per-rank count of pipelines that gave up)."""
+    n = len(inputs)
+    sends = [np.array(x, dtype=np.float32) for x in inputs]
+    recvs = [np.full_like(x, np.nan) for x in sends]
+    sp = (ctypes.c_void_p * n)(*[s.ctypes.data for s in sends])
+    rp = (ctypes.c_void_p * n)(*[r.ctypes.data for r in recvs])
+    sg = (ctypes.c_uint64 * n)(*sigs)
+    mm = (ctypes.c_int * n)()
+    rc = load().mnccl_sim_signed_read(sp, rp, n, sends[0].size, channels, slice_bytes, sg, seed, mm)
+    if rc == -1:
+        raise RuntimeError("simulated protocol deadlocked")
+    if rc not in (0, 1):
+        raise ValueError(f"bad simulator arguments (rc={rc})")
+    return recvs, list(mm)

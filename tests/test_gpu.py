@@ -352,6 +352,67 @@ def test_read_grid_skewed_and_interleaved(dev):
     _run_allreduce(n, cases, timeout=600)
 
 
+def _run_windows(n, scenario, env=None, timeout=300):
+    port = GW.free_port()
+    e = {"MINI_NCCL_TIMEOUT_MS": "20000", **(env or {})}
+    out = GW.run_ranks(GW.window_rank, n, lambda r: (r, n, port, e, scenario), timeout, barrier=True)
+    assert sorted(out) == list(range(n)), out
+    for r in range(n):
+        assert "error" not in out[r], out[r]["error"]
+        _check_placement(r, n, out[r]["info"], env)
+    return out
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_registered_windows_parity(dev, n):
+    # calls inside registered windows (same windows, same offsets on every rank) run
+    # the read schedule with no host rendezvous; every dtype class, in place and out of place,
+    # ragged counts, the grid form, interleaved with negotiated and ring calls: bit-exact vs the oracle
+    out = _run_windows(n, "parity", {"GPU_MAX_HW_QUEUES": "2"} if n > 4 else None, timeout=600)
+    for r in range(n):
+        o = out[r]
+        assert o["windows"] == 2 and o["windows_after"] == 0 and o["destroy"] == 0, o
+        assert all(rc == 0 for rc in o["rcs"]) and all(b == 0 for b in o["bad"]), (r, o["rcs"], o["bad"])
+        assert o["kinds"] == [2] * len(o["kinds"]), o["kinds"]  # the read schedule, every window call
+        assert o["wc"] == [1] * len(o["wc"]), o["wc"]           # ... each without a rendezvous
+        assert o["info"]["read_map_failures"] == 0 and o["info"]["ipc_open_failures"] == 0
+
+
+def test_registered_windows_host_independent(dev):
+    # MINI_NCCL_BLOCKING=0 and windows: rank 0's call returns while rank 1 still sleeps 50 ms before
+    # its own -- no host rendezvous -- and every result is bit-exact
+    out = _run_windows(2, "async", {"MINI_NCCL_BLOCKING": "0"})
+    o0, o1 = out[0], out[1]
+    assert o0["bad"] == [0] * 4 and o1["bad"] == [0] * 4, (o0["bad"], o1["bad"])
+    assert o0["window_calls"] == 4 and o1["window_calls"] == 4
+    print(f"\n[windows] rank 0 host time per call (rank 1 50 ms late): "
+          f"{[round(t * 1e6, 1) for t in o0['call_s']]} us")
+    assert max(o0["call_s"]) < 0.01, o0["call_s"]  # far below the 50 ms a rendezvous would wait
+
+
+def test_registered_windows_mismatch_is_invalid_usage(dev):
+    # a window call whose ranks pass different offsets: the kernels see the signatures differ at
+    # START and give up before touching a buffer -- ncclInvalidUsage on every rank, sticky
+    import mini_nccl as M
+    out = _run_windows(3, "mismatch")
+    for r in range(3):
+        o = out[r]
+        assert o["rc"] == M.ncclInvalidUsage and o["rc2"] == M.ncclInvalidUsage, (r, o)
+        assert o["secs"] < 5, o
+
+
+def test_registered_windows_unregistered_peer_fails_fast(dev):
+    # rank 0 passes window buffers, the others buffers outside any window: the others see rank 0's
+    # window record in their rendezvous and fail the call at once (ncclInvalidUsage), raising rank
+    # 0's ABORT so its kernel does not wait for a START that never comes
+    import mini_nccl as M
+    out = _run_windows(3, "unregistered")
+    for r in range(3):
+        o = out[r]
+        assert o["rc"] in (M.ncclInvalidUsage, M.ncclRemoteError), (r, o)
+        assert o["rc2"] != 0 and o["secs"] < 5, (r, o)
+
+
 def test_schedules_interleaved_on_one_communicator(dev):
     # the one-shot, the ring and the read schedule share the per-(pair, pipeline) FIFO counters,
     # READY words, credits and scratch slots: calls of all three (and auto's choice by size)

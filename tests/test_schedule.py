@@ -301,3 +301,30 @@ def test_topology_rule_for_the_default_schedule(sim_lib):
     # the diagonal (a rank and itself) never counts
     link, hops = _topo(3, kind=S.PCIE, devices=[0, 0, 0])
     assert S.topology_blocks_read(link, hops) is None
+
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_sim_registered_window_signatures_random_interleavings(sim_lib, n):
+    # a registered-window read call is launched with no host rendezvous; each
+    # rank's START carries the call's signature and every pipeline compares its peers' with its
+    # own before touching any buffer.  Under random interleavings: equal signatures -> the
+    # oracle's bits; any rank differing -> every pipeline of every rank gives up and no recv
+    # element is written (the call fails with ncclInvalidUsage instead of reading a wrong buffer)
+    import oracle_api as O
+    count = n * 2500 + 3
+    xs = O.random_inputs(n, count, "f32", seed=77)
+    exp = O.allreduce(xs, "f32", "sum")
+    for seed in range(1, 13):
+        out, mm = S.signed_read(xs, [0x5eed] * n, seed=seed)
+        assert mm == [0] * n
+        body = (count // n) * n
+        for r in range(n):
+            assert np.array_equal(out[r][:body].view(np.uint32), exp[r][:body].view(np.uint32)), (seed, r)
+        for bad_rank in {0, n - 1, seed % n}:
+            sigs = [0x5eed] * n
+            sigs[bad_rank] = 0x5eed + 2 * seed  # another window / offset / count on one rank
+            out, mm = S.signed_read(xs, sigs, seed=seed)
+            assert all(m > 0 for m in mm), (seed, bad_rank, mm)
+            assert len(set(mm)) == 1, mm  # every pipeline of every rank, alike
+            assert all(np.isnan(o).all() for o in out), (seed, bad_rank)  # nothing written
