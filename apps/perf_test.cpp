@@ -1,7 +1,7 @@
 // perf_test -- the reference's measurement harness (tests/perf_test.cpp:34-158) for the
 // MI355X build, written against the same C ABI (include/mini_nccl_api.h).
 //
-//   perf_test <rank> <n_ranks> [master_ip] [--mode device|host|staged] [--sizes MiB,MiB,...]
+//   perf_test <rank> <n_ranks> [master_ip] [--mode device|host|staged] [--sizes MiB,MiB,...] [--window]
 //
 // Same protocol as the reference: sizes 1/16/64/128 MiB fp32, every rank sends 1.0, 5
 // warm-up and 20 timed all-reduces between CLOCK_MONOTONIC reads, an AVX2 compare scan
@@ -11,8 +11,10 @@
 //   --mode host    the reference's own usage: pinned host buffers (cudaHostAlloc,
 //                  perf_test.cpp:78-79) handed straight to ncclAllReduce; the kernel reads
 //                  and writes them through their device mapping, i.e. the end-to-end rate
-//                  including PCIe (MINI_NCCL_STAGE_HOST=1: staged through HBM instead);
+//                  including PCIe;
 //   --mode staged  pinned host -> explicit H2D -> all-reduce -> D2H per call.
+//   --window       (device mode) register send and recv with mncclCommRegister first: the calls
+//                  then run with no host rendezvous (the Schedule column reads "read/win").
 // Device: rank % device_count (the reference pinned every rank to GPU 0, :46;
 // MINI_NCCL_PERF_DEVICE overrides).
 #include <hip/hip_runtime.h>
@@ -22,6 +24,8 @@
 // weak: the program also runs against a library without it (an older build, or another
 // implementation of the ABI), and prints "?" there
 extern "C" ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* info, size_t size) __attribute__((weak));
+extern "C" ncclResult_t mncclCommRegister(ncclComm_t comm, void* buff, size_t size, void** handle) __attribute__((weak));
+extern "C" ncclResult_t mncclCommDeregister(ncclComm_t comm, void* handle) __attribute__((weak));
 #include <immintrin.h>
 #include <time.h>
 #include <unistd.h>
@@ -83,6 +87,7 @@ int main(int argc, char** argv) {
   std::string mode = "device";
   std::vector<size_t> sizes = {1u << 20, 16u << 20, 64u << 20, 128u << 20};  // bytes
   int iters = 20, warmup = 5;
+  bool window = false;
   for (int a = 3; a < argc; ++a) {
     std::string s = argv[a];
     if (s == "--mode" && a + 1 < argc) mode = argv[++a];
@@ -95,6 +100,7 @@ int main(int argc, char** argv) {
       }
     } else if (s == "--iters" && a + 1 < argc) iters = atoi(argv[++a]);
     else if (s == "--warmup" && a + 1 < argc) warmup = atoi(argv[++a]);
+    else if (s == "--window") window = true;
     else ip = argv[a];
   }
   int ndev = 0;
@@ -123,6 +129,15 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < count; ++i) h_send[i] = 1.0f;  // perf_test.cpp:82
     memset(h_recv, 0, bytes);
     HIP_OK(hipMemcpy(d_send, h_send, bytes, hipMemcpyHostToDevice));
+    void *w_send = nullptr, *w_recv = nullptr;
+    if (window && mode == "device") {
+      if (!mncclCommRegister) {
+        fprintf(stderr, "--window: this library has no mncclCommRegister\n");
+        return 1;
+      }
+      NCCL_OK(mncclCommRegister(comm, d_send, bytes, &w_send));
+      NCCL_OK(mncclCommRegister(comm, d_recv, bytes, &w_recv));
+    }
 
     auto one = [&]() {
       if (mode == "staged") HIP_OK(hipMemcpyAsync(d_send, h_send, bytes, hipMemcpyHostToDevice, stream));
@@ -157,9 +172,12 @@ int main(int argc, char** argv) {
     mncclCommInfo_t info;
     memset(&info, 0, sizeof info);
     const char* sched = !mncclCommGetInfoV || mncclCommGetInfoV(comm, &info, sizeof info) != ncclSuccess ? "?"
-                        : info.last_algo == 0 ? "ring" : info.last_algo == 2 ? "read" : info.last_algo == 3 ? "oneshot" : "-";
+                        : info.last_algo == 0 ? "ring" : info.last_algo == 2 ? (w_send ? "read/win" : "read")
+                        : info.last_algo == 3 ? "oneshot" : "-";
     if (rank == 0) printf("%15zu %15.2f %15.2f %15.2f %9s %s\n", bytes, us, alg, bus, sched, bad >= 0 ? "(FAIL)" : "");
     fflush(stdout);
+    if (w_send) NCCL_OK(mncclCommDeregister(comm, w_send));
+    if (w_recv) NCCL_OK(mncclCommDeregister(comm, w_recv));
     HIP_OK(hipFree(d_send));
     HIP_OK(hipFree(d_recv));
     HIP_OK(hipHostFree(h_send));

@@ -464,9 +464,11 @@ def size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks, 
 def small_calls(M, torch, dist, comm, send, recv, stream, n, max_over_ranks, warm=10, reps=100):
     """us per blocking 4 KiB / 64 KiB fp32 call for each schedule (forced), all ranks in step:
     what auto's order for small calls (read first for shareable device buffers, the one-shot for
-    the ring's small calls) should be decided from on this topology"""
+    the ring's small calls) should be decided from on this topology; read_window: the read
+    schedule on registered windows (no host rendezvous)"""
     rows = []
-    names = {"ring": M.ALGO_RING, "read": M.ALGO_READ, "oneshot": M.ALGO_ONESHOT}
+    names = {"ring": M.ALGO_RING, "read": M.ALGO_READ, "oneshot": M.ALGO_ONESHOT, "read_window": M.ALGO_READ}
+    wins = None
     try:
         for kib in (4, 64):
             k = (kib << 10) // 4
@@ -474,6 +476,11 @@ def small_calls(M, torch, dist, comm, send, recv, stream, n, max_over_ranks, war
             row = {"KiB": kib}
             for name, a in names.items():
                 comm.set_algo(a)
+                if name == "read_window" and wins is None:
+                    # send / recv registered as windows (mncclCommRegister, collective): the same
+                    # calls with no host rendezvous
+                    wins = (comm.register(send.data_ptr(), send.numel() * send.element_size()),
+                            comm.register(recv.data_ptr(), recv.numel() * recv.element_size()))
 
                 def call():
                     rc = comm.all_reduce(s_.data_ptr(), r_.data_ptr(), k, M.ncclFloat, M.ncclSum, stream.cuda_stream)
@@ -489,12 +496,17 @@ def small_calls(M, torch, dist, comm, send, recv, stream, n, max_over_ranks, war
                     torch.cuda.synchronize()
                 dt = max_over_ranks(time.perf_counter() - t0) / reps
                 ran = comm.info()["last_algo"]
+                if name == "read_window" and comm.info()["window_calls"] < warm + reps:
+                    ran = -1  # not the window path: reported as a failed point
                 row[name + "_us"] = round(dt * 1e6, 1)
                 row[name + "_ok"] = max_over_ranks(0.0 if (ran == a and bool((r_ == float(n)).all().item()))
                                                    else 1.0) == 0.0
             rows.append(row)
     finally:
         comm.set_algo(M.ALGO_AUTO)
+        if wins is not None:
+            for h in wins:
+                comm.deregister(h)
     return rows
 
 

@@ -305,17 +305,18 @@ __device__ __forceinline__ bool wave_wait_peers(const u64* flag, u64 target, boo
 // peers' buffer addresses come from the windows every rank registered together, on the promise
 // that every rank passes the same windows, offsets, count, dtype and op.  The promise is checked
 // here, on the device, before any peer buffer is touched: START carries the caller's signature
-// (a hash of those) in word kSigWord of the READY line, stored and drained before the flag; after
-// every peer's START, lane q compares peer q's signature with this rank's and clears the word (a
-// later call can never match a stale one).  Any difference -- seen by every rank alike, as every
-// rank compares every pair it is part of -- gives up the call with kStatusMismatch (ncclInvalidUsage).
+// (a hash of those, never 0) in word kSigWord of the READY line, stored just before the flag (no
+// drain between the two: the signature may land after the flag).  After every peer's START, lane
+// q waits for peer q's signature word to be non-zero, compares it with this rank's and clears it
+// (so a later call never meets a stale one: a peer writes its next signature only after this
+// call's DONE).  Any difference -- seen by every rank alike, as every rank compares every pair it
+// is part of -- gives up the call with kStatusMismatch (ncclInvalidUsage).
 // The START of read_start_kernel; read_kernel writes the same stores inline, its flag value read
 // inside the peer-lane branch (read outside it, from a clamped LDS index, the persistent kernel's
 // fold spilled 36 registers to scratch at the 256-register bound).
 __device__ __forceinline__ void send_start(const CollParams& p, int C, int lane, u64 v, int w) {
   const int n = p.n, r = p.rank;
   if (lane < n && lane != r && p.sig) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w) + kSigWord, p.sig);
-  if (p.sig) drain_stores();  // the signature has landed before the flag can be seen
   if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), v);
 }
 
@@ -331,8 +332,11 @@ __device__ __noinline__ bool sig_differs(u64* word, u64 sig) {
 __device__ __forceinline__ bool starts_agree(const CollParams& p, const Ctl& c, int C, int lane, int w) {
   if (!p.sig) return true;
   const int n = p.n, r = p.rank;
+  const bool peer = lane < n && lane != r;
+  u64* word = p.mbox + mbox_ready(C, peer ? lane : 0, w) + kSigWord;
+  if (!wave_wait_peers(word, 1, peer, c, lane, false)) return false;  // (status set: timeout / abort)
   bool bad = false;
-  if (lane < n && lane != r) bad = sig_differs(p.mbox + mbox_ready(C, lane, w) + kSigWord, p.sig);
+  if (peer) bad = sig_differs(word, p.sig);
   if (__builtin_amdgcn_ballot_w64(bad) == 0) return true;
   if (lane == 0 && claim_first(c)) st_sys32(c.status, kStatusMismatch);
   return false;
@@ -845,9 +849,8 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
   // START to every peer (with the call's signature on a registered-window call), then wait for theirs
   if (lane < n && lane != r) {
     if (p.sig) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w) + kSigWord, p.sig);
+    st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + 1);
   }
-  if (p.sig) drain_stores();  // the signature has landed before the flag can be seen
-  if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + 1);
   if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), rx[lane < n ? lane : 0] + 1, lane < n && lane != r, ctl, lane,
                        true))
     goto aborted;

@@ -141,16 +141,21 @@ bool read_step(World& W, Prog& P) {
   };
   switch (P.j) {
     case 0:
-      // START (kernels.hip read_kernel): a registered-window call's signature lands first
-      if (!W.sig.empty())
-        for (int k = 1; k < n; ++k) W.mbox[direct_peer(n, r, k)][mbox_ready(W.C, r, w) + kSigWord] = W.sig[r];
+      // START (kernels.hip read_kernel).  A registered-window call's signature is stored with it but
+      // not drained first, so it may land after the flag: modelled as a later step (stage 5)
       for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx(direct_peer(n, r, k)) + 1;
+      P.j = W.sig.empty() ? 1 : 5;
+      return true;
+    case 5:
+      for (int k = 1; k < n; ++k) W.mbox[direct_peer(n, r, k)][mbox_ready(W.C, r, w) + kSigWord] = W.sig[r];
       P.j = 1;
       return true;
     case 1:
       for (int k = 1; k < n; ++k)
         if (W.ready(r, direct_peer(n, r, k), w) < rx(direct_peer(n, r, k)) + 1) return false;
-      if (!W.sig.empty()) {  // kernels.hip starts_agree: compare, clear, give up before any data
+      if (!W.sig.empty()) {  // kernels.hip starts_agree: wait for each signature, compare, clear
+        for (int k = 1; k < n; ++k)
+          if (W.mbox[r][mbox_ready(W.C, direct_peer(n, r, k), w) + kSigWord] == 0) return false;
         bool bad = false;
         for (int k = 1; k < n; ++k) {
           uint64_t& word = W.mbox[r][mbox_ready(W.C, direct_peer(n, r, k), w) + kSigWord];
