@@ -123,8 +123,16 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
                                                           nbytes + off, fresh)
             if not inplace:
                 recv.fill_byte(0xAB)
+            # "window": send / recv registered (mncclCommRegister, collective: every rank runs the
+            # same cases in the same order) for this case, deregistered after it
+            wins = []
+            if case.get("window"):
+                wins.append(comm.register(send.ptr, nbytes + off))
+                if not inplace:
+                    wins.append(comm.register(recv.ptr, nbytes + off))
             rc = 0
             grid0 = comm.info()["read_grid_calls"]
+            win0 = comm.info()["window_calls"]
             t0 = time.time()
             bad, first, detail = 0, -1, ""
             # "vary": new inputs every call, each call checked (a stale slot or flag from the
@@ -163,9 +171,12 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
             results.append({"case": case, "rc": rc, "bad": bad, "first": first, "detail": detail, "secs": dt,
                             "async": comm.async_error(), "last_algo": ci["last_algo"],
                             "grid_calls": ci["read_grid_calls"] - grid0,
+                            "window_calls": ci["window_calls"] - win0,
                             "peer_mappings": ci["peer_mappings"], "ipc_open_failures": ci["ipc_open_failures"],
                             "read_map_failures": ci["read_map_failures"], "closed_freed": ci["closed_freed"],
                             "live_exports": ci["live_exports"]})
+            for h in wins:
+                comm.deregister(h)
             send.free()
             if not inplace:
                 recv.free()

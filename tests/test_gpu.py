@@ -107,6 +107,8 @@ def _run_allreduce(n, cases, env=None, timeout=300, barrier=True):
                 assert res["last_algo"] == 3, f"rank {r} case {c}: ran schedule {res['last_algo']}"
             if "expect_algo" in c:
                 assert res["last_algo"] == c["expect_algo"], f"rank {r} case {c}: ran schedule {res['last_algo']}"
+            if c.get("window") and c["algo"] in (-1, 2, 4) and c["count"] >= n:  # no rendezvous, every call
+                assert res["window_calls"] == c["calls"], (r, c, res["window_calls"])
             if "expect_grid" in c:  # the read schedule's grid form ran every call of the case (or none)
                 assert res["grid_calls"] == (c["calls"] if c["expect_grid"] else 0), (r, c, res["grid_calls"])
             # no IPC open ever failed (nothing retries: a failure would send a call to the
@@ -419,9 +421,10 @@ def test_schedules_interleaved_on_one_communicator(dev):
     # alternate on one communicator, on changing data, every call checked
     n = 4
     plan = [(3, 3000), (0, 70001), (2, 1 << 18), (-1, 4096), (3, 16384), (0, 1000), (-1, 1 << 20), (2, 777),
-            (3, 100003), (-1, 65536 // 4), (0, 5), (3, 8 * 1024)]
-    # (auto: device buffers every rank shares run the read schedule at every size)
-    cases = [_case(count=c, algo=a, calls=2, vary=True, seed=800 + i, inplace=(i % 2 == 0),
+            (3, 100003), (-1, 65536 // 4), (0, 5), (3, 8 * 1024), (4, 4 * (1 << 20) + 3)]
+    # (auto: device buffers every rank shares run the read schedule at every size); five read /
+    # auto cases on registered windows (no host rendezvous for their calls)
+    cases = [_case(count=c, algo=a, calls=2, vary=True, seed=800 + i, inplace=(i % 2 == 0), window=i in (2, 3, 6, 7, 12),
                    **({"expect_algo": 2} if a == -1 else {})) for i, (a, c) in enumerate(plan)]
     _run_allreduce(n, cases, timeout=600)
 

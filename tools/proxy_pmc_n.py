@@ -40,7 +40,7 @@ def main():
     algos = sys.argv[4:] or ["ring", "read_push"]
     base = os.path.join(ROOT, "gpurun_out", tag)
     def fused_of(form):  # bench.py fused_bytes
-        return 4 * (COUNT // n) * {"ring": 6 * n - 4, "read_push": 2 * n, "read_load": 3 * n - 1}[form]
+        return 4 * (COUNT // n) * {"ring": 6 * n - 4, "read_push": 2 * n, "read_grid": 2 * n, "read_load": 3 * n - 1}[form]
     summ_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     summ = json.load(open(summ_path)) if os.path.exists(summ_path) else {}
     pmc_csv = os.path.join(ROOT, "profiles", f"{rnd}_proxy_pmc_n{n}.csv")
@@ -53,8 +53,9 @@ def main():
         for algo in algos:
             fused = fused_of(algo)
             # the kernel's template arguments name its form: read_kernel<float, 0, true, PUSH>
+            # (the grid form: its fold grid, read_grid_kernel<float, 0, G, V>; START / DONE are one wave each)
             k = {"ring": "ring_kernel<float, 0, true>", "read_push": "read_kernel<float, 0, true, true>",
-                 "read_load": "read_kernel<float, 0, true, false>"}[algo]
+                 "read_grid": "read_grid_kernel<float, 0,", "read_load": "read_kernel<float, 0, true, false>"}[algo]
             tr = rows(os.path.join(base, f"trace_{algo}_n{n}", "run_kernel_trace.csv"), k)
             durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr]
             md = med_after5(durs)

@@ -9,7 +9,7 @@ OUT=$R/gpurun_out/${1:-r2_prof_read}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 export MINI_NCCL_PERF_DEVICE=0 GPU_MAX_HW_QUEUES=2
-prof() {  # prof <n> <pass> <port> <form: ring | read | read_push | read_load> <rocprof args...>
+prof() {  # prof <n> <pass> <port> <form: ring | read | read_push | read_load | read_grid> <rocprof args...>
   local n=$1 pass=$2 port=$3 algo=$4; shift 4
   export MINI_NCCL_READ_PUSH=1
   [ $algo = read_load ] && export MINI_NCCL_READ_PUSH=0

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Mixed-schedule stress through the library: N rank processes on one GPU run CALLS all-reduces on
-ONE communicator, each call's schedule drawn from auto / ring / read (push form) / one-shot, its
+ONE communicator, each call's schedule drawn from auto / ring / read (push form) / one-shot / read's
+grid form, a quarter of the device-buffer calls on registered windows (no host rendezvous), its
 size from a few bytes to 16 MiB (one-shot's small calls, read's persistent and large slices, the
 ring's partial grids), its dtype and op from the whole matrix, in place or not, device / pinned
 host buffers, fresh allocations or cached ones, ranks entering out of step (0-3 ms skew) --
@@ -31,14 +32,16 @@ def main():
     n = a.ranks
     cases = []
     for i in range(a.calls):
-        algo = int(rng.choice([-1, 0, 2, 3]))
+        algo = int(rng.choice([-1, 0, 2, 3, 4]))
         dtype = str(rng.choice(["f32", "f64", "i32", "f16", "bf16"]))
         op = str(rng.choice(["sum", "prod", "max", "min"]))
-        count = int(rng.choice([n - 1, n, 77, 1000, 4099, 16384, 65536 + 3, 1 << 18, (1 << 20) + 5, 1 << 22]))
+        count = int(rng.choice([n - 1, n, 77, 1000, 4099, 16384, 65536 + 3, 1 << 18, (1 << 20) + 5, 1 << 22,
+                                n << 20]))
         mem = "pinned" if rng.random() < 0.1 else "device"
         cases.append(dict(dtype=dtype, op=op, count=count, inplace=bool(rng.random() < 0.3), algo=algo, calls=1,
                           seed=7000 + i, special=op in ("max", "min"), offset=0, mem=mem,
-                          fresh=bool(mem == "device" and rng.random() < 0.2), skew_ms=3))
+                          fresh=bool(mem == "device" and rng.random() < 0.2), skew_ms=3,
+                          window=bool(mem == "device" and rng.random() < 0.25)))
     port = GW.free_port()
     env = {"MINI_NCCL_TIMEOUT_MS": "30000", "GPU_MAX_HW_QUEUES": "2"}
     out = GW.run_ranks(GW.allreduce_rank, n, lambda r: (r, n, port, cases, env), 2400, barrier=True)
