@@ -896,7 +896,8 @@ def main():
             """MNCCL_BENCH_INJECT=<where>: rehearses the failure paths below (a GPU fault aborts the
             process: the armed line must still come out).  Stages after the ring: run_read (the
             headline), probe, standalone, rccl, sizes, small_calls, host_buffers, sweep; <stage>_error raises
-            an ncclInternalError there instead"""
+            an ncclInternalError there instead; verify_<algo> marks that schedule's results wrong on
+            rank 0 (run_algo)"""
             if os.environ.get("MNCCL_BENCH_INJECT") == where and rank == 0:
                 log(f"injected abort at {where}")
                 os.abort()
@@ -947,6 +948,9 @@ def main():
                 log(f"rank {rank}: {algo} calls ran {fallbacks[algo]['ran']}: {fallbacks[algo]}")
                 result["config"]["fallbacks"] = dict(fallbacks)
             ok = ok and ran_ok
+            if os.environ.get("MNCCL_BENCH_INJECT") == f"verify_{algo}" and rank == 0:
+                ok = False  # rehearses a wrong-result schedule (the line must fall back to the ring's number)
+                verifies.setdefault(algo, {})["order_sensitive"] = "FAILED: injected (MNCCL_BENCH_INJECT)"
             send.fill_(1.0)
             ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
             return max_over_ranks(wall), max_over_ranks(ev_ms), ok
@@ -1021,11 +1025,13 @@ def main():
         result["schedules"] = {}
         # 1. the reference's ring first (the north star's schedule, C3's "8 MI355X ring"): measured
         # and armed before the default, so a fault in the default still leaves a measured line
+        ring_meas = None
         if headline_algo != "ring":
             if rank == 0:
                 log("schedule ring (armed first)")
             try:
                 wr, er, okr = run_algo("ring")
+                ring_meas = (wr, er, okr)
                 result["schedules"]["ring"] = point("ring", wr, er, okr)
                 set_line("ring", wr, er, okr, note=f"PROVISIONAL: the ring's line; the default schedule "
                                                    f"({headline_algo}) was being measured when the process ended")
@@ -1038,6 +1044,15 @@ def main():
             wall, ev_ms, ok = run_algo(headline_algo, auto=auto_mode)
             result["schedules"][headline_algo] = point(headline_algo, wall, ev_ms, ok)
             algbw = set_line(headline_algo, wall, ev_ms, ok)
+            if not ok and ring_meas and ring_meas[2]:
+                # the default's results were wrong on some rank (verify_calls / verify_order): a
+                # number for wrong bits is no measurement -- the line carries the ring's (checked ok),
+                # the default's failure on record in schedules.<algo> and result_check
+                algbw = set_line("ring", *ring_meas,
+                                 note=f"FAILED: the default schedule ({headline_algo}) gave wrong results on some "
+                                      f"rank ({(result['schedules'][headline_algo].get('verify') or {}).get('order_sensitive')}); "
+                                      "value is the ring's")
+                result["config"]["headline_error"] = f"{headline_algo}: wrong results"
         except M.NcclError as e:
             # the default schedule failed (every rank's calls fail alike): the line says so
             # (result_check FAILED, headline_error) and carries the ring's number, measured on a
