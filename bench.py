@@ -879,6 +879,12 @@ def main():
             # auto: read where the topology rule allows it on every pair of ranks, else the ring
             # (schedule.h topology_blocks_read; the library decides, the line reports)
             args.algo = ("read" if info["auto_read"] else "ring") if info["algo"] < 0 else ALGO_NAMES[info["algo"]]
+            # ... its large calls in the grid form when every rank has a GPU of its own (auto_grid;
+            # schedule.h read_grid_fits: <= 8 ranks, chunks of >= 4 MiB in whole 16-byte vectors)
+            chunk_b = (count // n) * esz
+            if (args.algo == "read" and info["auto_grid"] and n <= 8 and chunk_b >= (4 << 20)
+                    and chunk_b % 16 == 0):
+                args.algo = "read_grid"
         headline_algo = args.algo
         send = torch.ones(count, device=dev, dtype=tdt)
         recv = torch.empty(count, device=dev, dtype=tdt)
@@ -1014,7 +1020,14 @@ def main():
                         "link instead of 2(n-1)/n through one link); the north star's ring is measured first and "
                         "beside it in schedules.ring with its own roofline and link fractions; headline_check "
                         "states whether this line's own numbers uphold that default"
-                        if headline_algo == "read" else f"{headline_algo} ({'forced by --algo' if not auto_mode else 'auto'})")
+                        if headline_algo == "read" else
+                        "the library default for device buffers when every rank has a GPU of its own (MINI_NCCL_ALGO="
+                        "auto -> read in its grid form: a one-wave START, a grid of one-batch workgroups that fold each "
+                        "KiB of the rank's chunk from the peers' send buffers in the ring's association order and push "
+                        "it into every peer's recv, a one-wave DONE); the persistent read kernel and the north star's "
+                        "ring are measured beside it (schedules.read, schedules.ring), headline_check compares them"
+                        if headline_algo == "read_grid" and auto_mode else
+                        f"{headline_algo} ({'forced by --algo' if not auto_mode else 'auto'})")
         # 0. a line exists before anything runs on the GPU: if the process dies (a GPU fault
         # aborts it), the armed line is printed
         result.update({"value": 0.0, "cpu_baseline": cpu_ring,
@@ -1094,18 +1107,22 @@ def main():
         # the rule behind the default, checked against this line's own numbers: read stays the
         # library default while it moves the buffer at least as fast as the reference's ring
         rd, rg = result["schedules"].get("read", {}), result["schedules"].get("ring", {})
+        gd = result["schedules"].get("read_grid", {})
         if "value" in rd and "value" in rg:
+            # the default's form of read: the grid form where auto chose it (every rank alone on its GPU)
+            dflt = gd if headline_algo == "read_grid" and "value" in gd else rd
+            other = rd if dflt is gd else gd
             result["config"]["headline_check"] = {
-                "rule": "read is the default while schedules.read.value >= schedules.ring.value (same buffers, "
-                        "same bits); otherwise this node should run MINI_NCCL_ALGO=ring",
+                "rule": "read (in the form auto chose) is the default while its value >= schedules.ring.value (same "
+                        "buffers, same bits); otherwise this node should run MINI_NCCL_ALGO=ring; the form auto chose "
+                        "should also be >= the other read form",
+                "default_form": "read_grid" if dflt is gd else "read",
                 "read_GBps": rd["value"], "ring_GBps": rg["value"], "read_over_ring": round(rd["value"] / rg["value"], 3),
-                "holds": rd["value"] >= rg["value"]}
-            gd = result["schedules"].get("read_grid", {})
+                "holds": dflt["value"] >= rg["value"]}
             if "value" in gd:
-                # the grid form (mncclAlgoReadGrid), measured beside on the same buffers: if it wins on
-                # the node, it is the candidate for the default there
-                result["config"]["headline_check"].update({"read_grid_GBps": gd["value"],
-                                                           "read_grid_over_read": round(gd["value"] / rd["value"], 3)})
+                result["config"]["headline_check"].update({
+                    "read_grid_GBps": gd["value"], "read_grid_over_read": round(gd["value"] / rd["value"], 3),
+                    "form_holds": dflt["value"] >= other["value"]})
         if rank == 0:
             arm(result)
         # 4. the xGMI roofline the schedules are bound by, after the schedules themselves: bytes

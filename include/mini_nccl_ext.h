@@ -34,7 +34,7 @@ extern "C" {
    401 the one-shot schedule (mncclAlgoOneShot; auto's small calls that would run the ring);
    500 auto runs the read schedule only where every pair of GPUs is one xGMI hop apart (or
    shares a GPU), mncclCommInfo_t grew (same prefix: auto_read, peer_link / peer_hops,
-   auto_reason, read_grid_calls, window_calls, windows), mncclAlgoReadGrid, registered windows
+   auto_reason, read_grid_calls, window_calls, windows, auto_grid), mncclAlgoReadGrid, registered windows
    (mncclCommRegister / mncclCommDeregister: read calls with no host rendezvous) */
 #define MNCCL_VERSION 500
 
@@ -42,8 +42,9 @@ extern "C" {
 typedef enum {
   mncclAlgoAuto = -1,  /* the library's default: read for device buffers every rank can share
                           when every pair of GPUs is one xGMI hop apart (or shares a GPU: see
-                          mncclCommInfo_t.auto_read); every other call one-shot when at most
-                          64 KiB, else the ring */
+                          mncclCommInfo_t.auto_read) -- its large calls in the grid form when every
+                          rank has a GPU of its own (auto_grid); every other call one-shot when at
+                          most 64 KiB, else the ring */
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
   mncclAlgoDirect = 1, /* removed in 400 (never faster than the ring); mncclCommSetAlgo and
                           MINI_NCCL_ALGO reject it */
@@ -126,6 +127,8 @@ typedef struct {
                                             form (mncclAlgoReadGrid) */
   unsigned long long window_calls;       /* calls launched on registered windows: no host rendezvous */
   int windows;                           /* windows registered on this communicator */
+  int auto_grid;                         /* 1: auto launches large read calls in the grid form
+                                            (mncclAlgoReadGrid's): every rank has a GPU of its own */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,

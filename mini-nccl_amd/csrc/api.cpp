@@ -195,6 +195,7 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
   info->read_grid_calls = c->read_grid_calls();
   info->window_calls = c->window_calls();
   info->windows = (int)c->windows();
+  info->auto_grid = c->auto_grid() ? 1 : 0;
   memcpy(out, &full, size < sizeof full ? size : sizeof full);
   return ncclSuccess;
 }

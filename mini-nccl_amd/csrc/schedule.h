@@ -276,6 +276,15 @@ MNCCL_HD int topology_blocks_read(int n, const int* link, const int* hops) {
   return 0;
 }
 
+// Every rank has a GPU of its own (no pair of ranks shares one): auto then launches its large
+// push-form read calls in the grid form (kernels.hip read_grid_kernel; Comm::classify_topology).
+MNCCL_HD bool every_rank_alone(int n, const int* link) {
+  for (int q = 0; q < n; ++q)
+    for (int p = 0; p < n; ++p)
+      if (p != q && link[q * n + p] == kPeerSameGpu) return false;
+  return true;
+}
+
 // Kernel status bits (host-mapped status word)
 // kStatusMismatch: a registered-window call whose ranks passed different windows / offsets / count /
 // dtype / op (the START signatures differ, read_kernel): no data was touched, the call fails with

@@ -59,7 +59,7 @@ class CommInfo(ctypes.Structure):
         # since mncclVersion 500
         ("auto_read", ctypes.c_int), ("peer_link", ctypes.c_int * 16), ("peer_hops", ctypes.c_int * 16),
         ("auto_reason", ctypes.c_char * 160), ("read_grid_calls", ctypes.c_ulonglong),
-        ("window_calls", ctypes.c_ulonglong), ("windows", ctypes.c_int),
+        ("window_calls", ctypes.c_ulonglong), ("windows", ctypes.c_int), ("auto_grid", ctypes.c_int),
     ]
 
 

@@ -25,6 +25,7 @@ def load():
         L.mnccl_read_slice.restype = u64
         L.mnccl_call_pipelines.argtypes = [u64, i, i]
         L.mnccl_topology_blocks_read.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.mnccl_every_rank_alone.argtypes = [i, ctypes.POINTER(i)]
         L.mnccl_sim_signed_read.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64,
                                             ctypes.POINTER(u64), u64, ctypes.POINTER(i)]
         L.mnccl_oneshot_slice.argtypes = [u64, i, i, u64]
@@ -143,3 +144,10 @@ def signed_read(inputs, sigs, slice_bytes=1024, channels=4, seed=1):
     if rc not in (0, 1):
         raise ValueError(f"bad simulator arguments (rc={rc})")
     return recvs, list(mm)
+
+
+def every_rank_alone(link):
+    """csrc/schedule.h every_rank_alone: no pair of ranks shares a GPU (auto's grid form)."""
+    n = len(link)
+    flat = (ctypes.c_int * (n * n))(*[link[q][p] for q in range(n) for p in range(n)])
+    return bool(load().mnccl_every_rank_alone(n, flat))

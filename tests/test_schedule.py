@@ -328,3 +328,13 @@ def test_sim_registered_window_signatures_random_interleavings(sim_lib, n):
             assert all(m > 0 for m in mm), (seed, bad_rank, mm)
             assert len(set(mm)) == 1, mm  # every pipeline of every rank, alike
             assert all(np.isnan(o).all() for o in out), (seed, bad_rank)  # nothing written
+
+
+
+def test_auto_grid_form_only_when_every_rank_has_its_own_gpu(sim_lib):
+    # auto's large read calls take the grid form on a node (one rank per GPU), never when ranks share
+    # a GPU (8 co-located ranks: 0.61x the persistent kernel, profiles/r5_bench_n8_same_gpu.json)
+    assert S.every_rank_alone(_topo(8)[0])
+    assert S.every_rank_alone(_topo(2, kind=S.PCIE)[0])
+    assert not S.every_rank_alone(_topo(8, devices=[0] * 8)[0])
+    assert not S.every_rank_alone(_topo(4, devices=[0, 0, 1, 2])[0])
