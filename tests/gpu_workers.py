@@ -409,11 +409,15 @@ def graph_rank(rank, n, port, env, replays, out_q):
         st = hip_rt.Stream()
         count = int(env.get("GRAPH_COUNT", (1 << 18) + 1))
         send, recv = hip_rt.DeviceBuffer(count * 4), hip_rt.DeviceBuffer(count * 4)
+        if env.get("GRAPH_WINDOW") == "1":  # the captured call on registered windows (no rendezvous)
+            comm.register(send.ptr, count * 4)
+            comm.register(recv.ptr, count * 4)
         rcs = []
         g = hip_rt.Graph(st, lambda: rcs.append(comm.all_reduce(send.ptr, recv.ptr, count, M.ncclFloat, M.ncclSum,
                                                                 st.handle)))
         captured_algo = comm.info()["last_algo"]  # the schedule baked into the graph
         captured_grid = comm.info()["read_grid_calls"]
+        captured_window = comm.info()["window_calls"]
         bad = []
         for k in range(replays):
             xs = O.random_inputs(n, count, "f32", seed=500 + k)
@@ -432,7 +436,7 @@ def graph_rank(rank, n, port, env, replays, out_q):
         exp = O.allreduce(xs, "f32", "sum")[rank]
         g.destroy()
         out_q.put((rank, {"capture_rc": rcs, "bad": bad, "eager_rc": rc, "captured_algo": captured_algo,
-                          "captured_grid": captured_grid,
+                          "captured_grid": captured_grid, "captured_window": captured_window,
                           "eager_bad": int((got.view(np.uint32) != exp.view(np.uint32)).sum())}))
         send.free()
         recv.free()

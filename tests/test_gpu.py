@@ -635,15 +635,17 @@ def test_late_peer_is_aborted_fast(dev, algo):
     assert out[1]["secs"] < 1.5, out[1]  # well under its own 1.5 s watchdog + 2 s host limit
 
 
-@pytest.mark.parametrize("algo", ["ring", "read", "oneshot", "read_grid"])
+@pytest.mark.parametrize("algo", ["ring", "read", "oneshot", "read_grid", "read_window"])
 def test_allreduce_hip_graph_capture_and_replay(dev, algo):
     # the reference only warns under capture (api.cpp:153-166); here a captured all-reduce
     # replays correctly because the FIFO counters are device state advanced by the kernel (the
     # grid form: three captured launches, its `go` word rewritten by every replay's START)
     port = GW.free_port()
-    env = {"MINI_NCCL_TIMEOUT_MS": "20000", "MINI_NCCL_ALGO": algo}
+    env = {"MINI_NCCL_TIMEOUT_MS": "20000", "MINI_NCCL_ALGO": algo.replace("_window", "")}
     if algo == "read_grid":
         env["GRAPH_COUNT"] = str(3 * (1 << 20) + 1)
+    if algo == "read_window":  # registered windows: the captured launch carries its START signature
+        env["GRAPH_WINDOW"] = "1"
     out = GW.run_ranks(GW.graph_rank, 3, lambda r: (r, 3, port, env, 4), 240)
     assert sorted(out) == [0, 1, 2], out
     for r in range(3):
@@ -652,8 +654,9 @@ def test_allreduce_hip_graph_capture_and_replay(dev, algo):
         assert out[r]["bad"] == [0, 0, 0, 0]
         assert out[r]["eager_rc"] == 0 and out[r]["eager_bad"] == 0
         # the read schedule is captured too (its peer mappings pinned for the replays)
-        assert out[r]["captured_algo"] == {"ring": 0, "read": 2, "oneshot": 3, "read_grid": 2}[algo]
+        assert out[r]["captured_algo"] == {"ring": 0, "read": 2, "oneshot": 3, "read_grid": 2, "read_window": 2}[algo]
         assert out[r]["captured_grid"] == (1 if algo == "read_grid" else 0)
+        assert out[r]["captured_window"] == (1 if algo == "read_window" else 0)
 
 
 @pytest.mark.parametrize("algo", ["ring", "read", "oneshot"])
