@@ -303,9 +303,11 @@ int mnccl_topology_blocks_read(int n, const int* link, const int* hops) { return
 int mnccl_every_rank_alone(int n, const int* link) { return every_rank_alone(n, link) ? 1 : 0; }
 
 // Runs `calls` consecutive all-reduces (send -> recv, fp32; send == recv for in place) on n
-// simulated ranks with the GPU kernels' protocol; call i uses schedule (algo >> 2i) & 3 (0 ring,
-// 1 one-shot, 2 read in its push form, 3 read in its load form; schedules can alternate on one
-// communicator state, as mncclCommSetAlgo allows).  A one-shot call's slice: oneshot_slice when
+// simulated ranks with the GPU kernels' protocol; call i uses schedule (algo >> 3i) & 7 (0 ring,
+// 1 one-shot, 2 read in its push form, 3 read in its load form, 4 read's grid form -- START and
+// DONE on pipeline 0, the whole chunk folded and pushed between them, as kernels.hip
+// read_start / read_grid / read_done do; schedules can alternate on one communicator state, as
+// mncclCommSetAlgo allows; at most 21 calls).  A one-shot call's slice: oneshot_slice when
 // min_slice != 0 (Comm::launch; -2 if the call does not fit), else the slot.  schedule_seed != 0 permutes the order programs are tried
 // in (pseudo-random), exploring different interleavings.  min_slice: 0 = fixed payload (the
 // configured slice), else the adaptive payload of Comm::launch.  Returns 0, -1 on deadlock,
@@ -328,9 +330,10 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
   uint64_t steps = 0;
   uint64_t rng = schedule_seed * 6364136223846793005ull + 1442695040888963407ull;
   for (int call = 0; call < calls; ++call) {
-    const int code = (int)((algo >> (2 * call)) & 3);
+    const int code = (int)((algo >> (3 * call)) & 7);
+    if (code > 4) return -2;
     const int a = code >= 2 ? 2 : code;  // 0 ring, 1 one-shot, 2 read
-    W.push = code == 2;
+    W.push = code == 2 || code == 4;
     // as Comm::launch: adaptive payload (min_slice 0 = off; the read schedule's own rule), fixed
     // slot stride, one pipeline per slice up to all of them
     if (a == 1 && W.chunk_bytes) {
@@ -340,6 +343,7 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
     } else if (!min_slice || a == 1) W.slice = slice_bytes;
     else if (a == 2) W.slice = read_slice(W.chunk_bytes, channels, slice_bytes, min_slice, kReadDepth);
     else W.slice = effective_slice(W.chunk_bytes, channels, slice_bytes, min_slice, 1);
+    if (code == 4 && W.chunk_bytes) W.slice = W.chunk_bytes;  // grid form: one "slice", pipeline 0's protocol
     W.nslices = (W.chunk_bytes + W.slice - 1) / W.slice;
     W.A = call_pipelines(a == 1 ? W.nslices * (uint64_t)n : W.nslices, channels, 1);  // one-shot: per chunk too
     W.iters = (uint32_t)((W.nslices + (uint64_t)W.A - 1) / (uint64_t)W.A);

@@ -40,22 +40,22 @@ def load():
     return _lib
 
 
-# schedules: the ring, the one-shot, read in its push form, read in its load form
-RING, ONESHOT, READ, READ_LOAD = 0, 1, 2, 3
+# schedules: the ring, the one-shot, read in its push form, read in its load form, read's grid form
+RING, ONESHOT, READ, READ_LOAD, READ_GRID = 0, 1, 2, 3, 4
 
 
 def allreduce(inputs, algo=0, op=0, slice_bytes=1024, channels=4, slots=2, calls=1, seed=0, algos=None, min_slice=0,
               inplace=False):
     """fp32 all-reduce of `inputs` (one array per rank) through the simulated kernels,
-    `calls` times on one communicator state (schedule `algo` -- RING, READ (push form) or
-    READ_LOAD (MINI_NCCL_READ_PUSH=0) -- for every call, or the per-call list `algos`; at most 32
-    calls).  inplace: send == recv (then every call after the first reduces the previous
+    `calls` times on one communicator state (schedule `algo` -- RING, ONESHOT, READ (push form),
+    READ_LOAD (MINI_NCCL_READ_PUSH=0) or READ_GRID (the push form's grid launches) -- for every
+    call, or the per-call list `algos`; at most 21 calls).  inplace: send == recv (then every call after the first reduces the previous
     result).  Returns (outputs, steps); raises RuntimeError on deadlock."""
     if algos is None:
         algos = [algo] * calls
     calls = len(algos)
-    assert calls <= 32
-    mask = sum((a & 3) << (2 * i) for i, a in enumerate(algos))
+    assert calls <= 21
+    mask = sum((a & 7) << (3 * i) for i, a in enumerate(algos))
     n = len(inputs)
     sends = [np.array(x, dtype=np.float32) for x in inputs]  # own copies (in place writes them)
     recvs = sends if inplace else [np.full_like(x, np.nan) for x in sends]

@@ -338,3 +338,24 @@ def test_auto_grid_form_only_when_every_rank_has_its_own_gpu(sim_lib):
     assert S.every_rank_alone(_topo(2, kind=S.PCIE)[0])
     assert not S.every_rank_alone(_topo(8, devices=[0] * 8)[0])
     assert not S.every_rank_alone(_topo(4, devices=[0, 0, 1, 2])[0])
+
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+def test_sim_grid_form_between_other_schedules(oracle_lib, sim_lib, n):
+    # the grid form's protocol (START / DONE on pipeline 0 only, the whole chunk folded and pushed
+    # between them) interleaved with every other schedule on one communicator state, under random
+    # interleavings: every call bit-exact vs the oracle, no deadlock (the other pipelines' counters
+    # stay in step because every rank skips them alike)
+    import oracle_api as O
+    plans = [[S.READ_GRID, S.RING, S.READ_GRID, S.READ, S.ONESHOT, S.READ_GRID],
+             [S.READ, S.READ_GRID, S.READ_LOAD, S.READ_GRID, S.RING, S.READ]]
+    for i, algos in enumerate(plans):
+        count = n * 700 + i
+        xs = O.random_inputs(n, count, "f32", seed=60 + i)
+        ref = O.allreduce(xs, "f32", "sum")
+        for seed in range(1, 6):
+            got, _ = S.allreduce(xs, slice_bytes=16384, min_slice=1024, channels=64, slots=2, algos=algos, seed=seed)
+            body = (count // n) * n
+            for r in range(n):
+                assert np.array_equal(got[r][:body].view(np.uint32), ref[r][:body].view(np.uint32)), (algos, seed, r)
