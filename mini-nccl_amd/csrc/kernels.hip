@@ -1006,6 +1006,10 @@ __global__ void __launch_bounds__(64) read_grid_kernel(CollParams p) {
   drain_stores();  // every push acknowledged by the peer's memory before this wave ends
 }
 
+#ifndef MNCCL_GRID_V
+#define MNCCL_GRID_V 1
+#endif
+
 __global__ void __launch_bounds__(64) read_done_kernel(CollParams p) {
   if (*p.go != p.call_seq) return;  // START failed and already raised the peers' ABORT words
   const int lane = threadIdx.x, n = p.n, r = p.rank, C = p.pipes;
@@ -1350,9 +1354,10 @@ static hipError_t oneshot_for_t(int op, bool vec, int C, int nt, const CollParam
 
 template <typename T>
 static hipError_t read_grid_for_t(int op, const CollParams& p, hipStream_t st) {
-  const unsigned blocks = (unsigned)((p.chunk_bytes + 1023) / 1024);  // V = 1: 1 KiB per workgroup
+  constexpr int GV = MNCCL_GRID_V;  // 16-byte vectors per lane per workgroup: GV KiB of the chunk each
+  const unsigned blocks = (unsigned)((p.chunk_bytes + 1024 * GV - 1) / (1024 * GV));
   const int n = p.n;
-#define GRID_G(OPC, G) hipLaunchKernelGGL((read_grid_kernel<T, OPC, G, 1>), dim3(blocks), dim3(64), 0, st, p)
+#define GRID_G(OPC, G) hipLaunchKernelGGL((read_grid_kernel<T, OPC, G, GV>), dim3(blocks), dim3(64), 0, st, p)
 #define GRID_CASE(OPC)                    \
   case OPC:                               \
     if (n == 2) GRID_G(OPC, 1);           \
