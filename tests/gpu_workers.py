@@ -390,7 +390,8 @@ def fullsize_rank(rank, n, port, env, dtype, count, algos, out_q, barrier=None):
         send.free()
         recv.free()
         stream.destroy()
-        out_q.put((rank, {"results": res, "destroy": comm.destroy()}))
+        info = comm.info()
+        out_q.put((rank, {"results": res, "info": info, "destroy": comm.destroy()}))
     except Exception:
         out_q.put((rank, {"error": traceback.format_exc()}))
 
