@@ -1006,10 +1006,6 @@ __global__ void __launch_bounds__(64) read_grid_kernel(CollParams p) {
   drain_stores();  // every push acknowledged by the peer's memory before this wave ends
 }
 
-#ifndef MNCCL_GRID_V
-#define MNCCL_GRID_V 1
-#endif
-
 __global__ void __launch_bounds__(64) read_done_kernel(CollParams p) {
   if (*p.go != p.call_seq) return;  // START failed and already raised the peers' ABORT words
   const int lane = threadIdx.x, n = p.n, r = p.rank, C = p.pipes;
@@ -1354,16 +1350,17 @@ static hipError_t oneshot_for_t(int op, bool vec, int C, int nt, const CollParam
 
 template <typename T>
 static hipError_t read_grid_for_t(int op, const CollParams& p, hipStream_t st) {
-  constexpr int GV = MNCCL_GRID_V;  // 16-byte vectors per lane per workgroup: GV KiB of the chunk each
-  const unsigned blocks = (unsigned)((p.chunk_bytes + 1024 * GV - 1) / (1024 * GV));
-  const int n = p.n;
-#define GRID_G(OPC, G) hipLaunchKernelGGL((read_grid_kernel<T, OPC, G, GV>), dim3(blocks), dim3(64), 0, st, p)
+  // V 16-byte vectors per lane per workgroup: V KiB of the chunk each (schedule.h read_grid_vectors)
+  const int n = p.n, V = read_grid_vectors(n);
+  const unsigned blocks = (unsigned)((p.chunk_bytes + 1024u * V - 1) / (1024u * V));
+#define GRID_G(OPC, G, V) hipLaunchKernelGGL((read_grid_kernel<T, OPC, G, V>), dim3(blocks), dim3(64), 0, st, p)
 #define GRID_CASE(OPC)                    \
   case OPC:                               \
-    if (n == 2) GRID_G(OPC, 1);           \
-    else if (n == 3) GRID_G(OPC, 2);      \
-    else if (n <= 5) GRID_G(OPC, 4);      \
-    else GRID_G(OPC, 7);                  \
+    if (n == 2) GRID_G(OPC, 1, 1);        \
+    else if (n == 3) GRID_G(OPC, 2, 1);   \
+    else if (n == 4) GRID_G(OPC, 4, 1);   \
+    else if (n == 5) GRID_G(OPC, 4, 2);   \
+    else GRID_G(OPC, 7, 2);               \
     break;
   switch (op) {
     GRID_CASE(kSum) GRID_CASE(kProd) GRID_CASE(kMax) GRID_CASE(kMin)
@@ -1377,7 +1374,7 @@ static hipError_t read_grid_for_t(int op, const CollParams& p, hipStream_t st) {
 hipError_t launch_read_grid(int dtype, int op, const CollParams& p, hipStream_t st) {
   // the shapes the grid kernel assumes, checked before anything is launched
   if (p.n < 2 || p.n > 8 || p.chunk_bytes % 16 || !p.go || !read_grid_fits(p.chunk_bytes, p.n) ||
-      (p.chunk_bytes + 1023) / 1024 > 0x7fffffffull)
+      (p.chunk_bytes + 1023) / 1024 > 0x7fffffffull || (read_grid_vectors(p.n) != 1 && read_grid_vectors(p.n) != 2))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(read_start_kernel, dim3(1), dim3(64), 0, st, p);
   hipError_t e = hipGetLastError();

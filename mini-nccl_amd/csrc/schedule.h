@@ -180,6 +180,11 @@ constexpr uint64_t kReadGridMin = 4ull << 20;
 MNCCL_HD bool read_grid_fits(uint64_t chunk_bytes, int n) {
   return n >= 2 && n <= 8 && chunk_bytes >= kReadGridMin && chunk_bytes % 16 == 0;
 }
+// 16-byte vectors per lane in one grid workgroup (V KiB of the chunk, from every peer): one up to
+// 4 ranks, two from 5 (profiles/r5_grid_v_ab.txt, 1 GiB per rank on the one-GPU proxy: 8 ranks
+// 3.07 vs 4.72 ms per call with V = 2 vs 1 -- as fast as the persistent kernel -- while 2 and 4
+// ranks are 7 % and 3 % faster with V = 1)
+MNCCL_HD int read_grid_vectors(int n) { return n <= 4 ? 1 : 2; }
 
 // Scratch layout: one region per PEER rank (n - 1 of them: the owner never sends to itself),
 // [C][slots][slice_bytes] each.  region_index maps a peer rank q != owner to its region.
