@@ -35,8 +35,10 @@ extern "C" {
    500 auto runs the read schedule only where every pair of GPUs is one xGMI hop apart (or
    shares a GPU), mncclCommInfo_t grew (same prefix: auto_read, peer_link / peer_hops,
    auto_reason, read_grid_calls, window_calls, windows, auto_grid), mncclAlgoReadGrid, registered windows
-   (mncclCommRegister / mncclCommDeregister: read calls with no host rendezvous) */
-#define MNCCL_VERSION 500
+   (mncclCommRegister / mncclCommDeregister: read calls with no host rendezvous);
+   501 imports of a same-GPU peer's memory are never unmapped while the process lives (the GPU
+   driver's handle loss), mncclCommInfo_t grew (same prefix: retired_imports) */
+#define MNCCL_VERSION 501
 
 /* schedules; all produce bit-identical results (same fold order per element) */
 typedef enum {
@@ -129,6 +131,10 @@ typedef struct {
   int windows;                           /* windows registered on this communicator */
   int auto_grid;                         /* 1: auto launches large read calls in the grid form
                                             (mncclAlgoReadGrid's): every rank has a GPU of its own */
+  /* since 501 */
+  int retired_imports;                   /* process-wide: peers' freed allocations on this GPU still
+                                            mapped here (same-GPU ranks only; held until the process
+                                            exits -- DESIGN.md, Same-GPU handle loss) */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,

@@ -196,6 +196,7 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
   info->window_calls = c->window_calls();
   info->windows = (int)c->windows();
   info->auto_grid = c->auto_grid() ? 1 : 0;
+  info->retired_imports = (int)mnccl::ipc::retired_imports();
   memcpy(out, &full, size < sizeof full ? size : sizeof full);
   return ncclSuccess;
 }

@@ -27,8 +27,10 @@ struct Export {
 };
 struct Import {
   uint64_t owner, base, id;
-  void* map;    // the dma-buf's mapping (unmapped on close)
-  char* local;  // map + the owner's bo_off: the owner's base
+  void* map;      // the dma-buf's mapping (unmapped on close)
+  char* local;    // map + the owner's bo_off: the owner's base
+  bool same_gpu;  // the owner's memory is on this process's GPU (close_import retires it)
+  bool retired;   // its owner freed it; kept mapped until comm_closed (ipcreg.h close_import)
 };
 struct BlockImport {
   uint64_t owner, base, id;
@@ -67,7 +69,7 @@ std::string err_str(const char* what, hsa_status_t e) {
   const char* m = nullptr;
   if (hsa_status_string(e, &m) != HSA_STATUS_SUCCESS || !m) m = "unknown status";
   char b[256];
-  snprintf(b, sizeof b, "%s: HSA status 0x%x (%s)", what, (unsigned)e, m);
+  snprintf(b, sizeof b, "%s: HSA status 0x%x (%.80s)", what, (unsigned)e, m);
   return b;
 }
 
@@ -91,6 +93,15 @@ hsa_status_t match_agent(hsa_agent_t a, void* arg) {
     return HSA_STATUS_INFO_BREAK;
   }
   return HSA_STATUS_SUCCESS;
+}
+
+// An agent's PCI location, as Shared::gpu carries it (0 if unknown)
+uint32_t agent_location(hsa_agent_t a) {
+  uint32_t bdf = 0, dom = 0;
+  if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) != HSA_STATUS_SUCCESS ||
+      hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) != HSA_STATUS_SUCCESS)
+    return 0;
+  return (dom << 16) | (bdf & 0xfff8u);
 }
 
 // The HSA agent of this thread's current HIP device (HIP runs on the same runtime).  Caller holds
@@ -177,9 +188,13 @@ bool export_allocation(uint64_t base, uint64_t id, uint64_t size, Shared* d, std
   }
   int fd = -1;
   uint64_t off = 0;
+  errno = 0;
   const hsa_status_t e = hsa_amd_portable_export_dmabuf((const void*)(uintptr_t)base, size, &fd, &off);
   if (e != HSA_STATUS_SUCCESS) {
-    if (why) *why = err_str("hsa_amd_portable_export_dmabuf", e);
+    const int err = errno;  // the export ioctl's, when it failed there
+    if (why)
+      *why = err_str("hsa_amd_portable_export_dmabuf", e) + " (errno " + std::to_string(err) + ": " + strerror(err) +
+             "; " + std::to_string(s.exports.size()) + " exports live, " + std::to_string(size) + " bytes)";
     return false;
   }
   struct stat sb;
@@ -188,8 +203,19 @@ bool export_allocation(uint64_t base, uint64_t id, uint64_t size, Shared* d, std
     if (why) *why = std::string("fstat of an exported dma-buf: ") + strerror(errno);
     return false;
   }
+  // a dma-buf's size is its buffer object's: one too small to hold the allocation at `off` is not
+  // this allocation's (the same-GPU handle reuse of profiles/r5_export_reuse.txt can hand the export
+  // another object's handle) -- refused, the calls run the ring
+  const off_t end = lseek(fd, 0, SEEK_END);
+  if (end >= 0 && (uint64_t)end < off + size) {
+    hsa_amd_portable_close_dmabuf(fd);
+    if (why)
+      *why = "the exported dma-buf (" + std::to_string((long long)end) + " bytes) cannot hold the allocation (" +
+             std::to_string(size) + " bytes at offset " + std::to_string(off) + ")";
+    return false;
+  }
   d->fd = fd;
-  d->pad = 0;
+  d->gpu = agent_location(a);
   d->ino = (uint64_t)sb.st_ino;
   d->bo_off = off;
   s.exports.push_back(Export{base, id, size, *d});
@@ -260,7 +286,7 @@ char* find_import(uint64_t owner, uint64_t base, uint64_t id) {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
   for (const Import& m : s.imports)
-    if (m.owner == owner && m.base == base && m.id == id) return m.local;
+    if (!m.retired && m.owner == owner && m.base == base && m.id == id) return m.local;
   return nullptr;
 }
 
@@ -268,7 +294,7 @@ char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shar
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
   for (const Import& m : s.imports)
-    if (m.owner == owner && m.base == base && m.id == id) {
+    if (!m.retired && m.owner == owner && m.base == base && m.id == id) {
       if (fd >= 0) close(fd);
       return m.local;
     }
@@ -297,7 +323,8 @@ char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shar
     return nullptr;
   }
   char* local = (char*)p + d.bo_off;
-  s.imports.push_back(Import{owner, base, id, p, local});
+  const uint32_t here = agent_location(agent);
+  s.imports.push_back(Import{owner, base, id, p, local, here != 0 && here == d.gpu, false});
   return local;
 }
 
@@ -305,7 +332,11 @@ bool close_import(uint64_t owner, uint64_t base, uint64_t id) {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
   for (size_t i = 0; i < s.imports.size(); ++i)
-    if (s.imports[i].owner == owner && s.imports[i].base == base && s.imports[i].id == id) {
+    if (!s.imports[i].retired && s.imports[i].owner == owner && s.imports[i].base == base && s.imports[i].id == id) {
+      if (s.imports[i].same_gpu) {  // see ipcreg.h: unmapped by comm_closed
+        s.imports[i].retired = true;
+        return true;
+      }
       hsa_amd_interop_unmap_buffer(s.imports[i].map);
       s.imports.erase(s.imports.begin() + (long)i);
       return true;
@@ -316,7 +347,13 @@ bool close_import(uint64_t owner, uint64_t base, uint64_t id) {
 size_t imports() {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
-  return s.imports.size();
+  return (size_t)std::count_if(s.imports.begin(), s.imports.end(), [](const Import& m) { return !m.retired; });
+}
+
+size_t retired_imports() {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  return (size_t)std::count_if(s.imports.begin(), s.imports.end(), [](const Import& m) { return m.retired; });
 }
 
 void note_cap_refusal(const std::string& what) {
@@ -361,9 +398,11 @@ void comm_closed(const std::vector<uint64_t>& owners) {
       if (s.owner_refs[i].first != o) continue;
       if (--s.owner_refs[i].second > 0) break;
       s.owner_refs.erase(s.owner_refs.begin() + (long)i);
-      // no live communicator of this process talks to that owner any more: its imports go
+      // no live communicator of this process talks to that owner any more: its imports go --
+      // except imports of this GPU's memory, which stay mapped while the process lives (ipcreg.h
+      // close_import: their unmap would be a second delete of the owner's handle, whoever went first)
       for (size_t j = 0; j < s.imports.size();) {
-        if (s.imports[j].owner == o) {
+        if (s.imports[j].owner == o && !s.imports[j].same_gpu) {
           hsa_amd_interop_unmap_buffer(s.imports[j].map);
           s.imports.erase(s.imports.begin() + (long)j);
         } else {

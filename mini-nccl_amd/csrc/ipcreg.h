@@ -34,7 +34,7 @@ namespace ipc {
 // One exported allocation, as its owner holds it (fd) and publishes it (ino, bo_off).
 struct Shared {
   int32_t fd;       // the dma-buf descriptor in the owner's table, open while the allocation lives
-  int32_t pad;
+  uint32_t gpu;     // the owner's GPU (PCI domain << 16 | bus << 8 | device << 3): see close_import
   uint64_t ino;     // the dma-buf's inode: what a received duplicate must name
   uint64_t bo_off;  // the allocation base's offset inside the dma-buf
 };
@@ -64,9 +64,16 @@ char* find_import(uint64_t owner, uint64_t base, uint64_t id);
 // always closes (a cached import is returned as is); nullptr on failure (*why set).
 char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shared& d, std::string* why);
 // Unmaps an import whose owner freed the allocation; the caller makes sure no kernel of this
-// process still reads through it.  False if there was none.
+// process still reads through it.  False if there was none.  An import of memory of this process's
+// OWN GPU is retired instead -- never found again, kept mapped while the process lives (comm_closed
+// keeps same-GPU imports too): the GPU driver gives a same-GPU import the exporter's buffer-object
+// handle, so the owner's free and this unmap would delete that handle twice, and a buffer
+// allocated in between loses it -- its later export fails or, worse, names another buffer
+// (profiles/r5_export_alias.txt; DESIGN.md *Same-GPU handle loss*).  The second delete is left to
+// the process's exit.  Retired mappings count against the import cap.
 bool close_import(uint64_t owner, uint64_t base, uint64_t id);
-size_t imports();
+size_t imports();          // live imports
+size_t retired_imports();  // same-GPU imports of freed allocations, held until the process exits
 uint64_t open_failures();  // user-buffer imports that failed in this process
 // Exports (kMaxExports, 512) and imports (peerbuf.cpp kMaxImports, 1024) are capped per process;
 // a refused one sends its call to the ring.  Counted here, warned about once per process.
@@ -75,7 +82,8 @@ uint64_t cap_refusals();
 
 // Communicator lifecycle.  Every live communicator registers the process nonces of its peers
 // in other processes; comm_closed (once no kernel of the closing communicator runs) closes this
-// process's imports of an owner no other live communicator shares, and -- when it was the last
+// process's imports of an owner no other live communicator shares (other GPUs' memory only, see
+// close_import), and -- when it was the last
 // live communicator of the process -- this process's exports too, so memory a caller frees
 // after its last communicator is gone is released at once (the dma-bufs held it).
 void comm_opened(const std::vector<uint64_t>& owners);

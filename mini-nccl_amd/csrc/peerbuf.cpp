@@ -316,7 +316,7 @@ char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, int fd, const ipc
     if (fd >= 0) close(fd);
     return p;
   }
-  if (ipc::imports() >= kMaxImports) {
+  if (ipc::imports() + ipc::retired_imports() >= kMaxImports) {
     if (fd >= 0) close(fd);
     *why = "the process maps " + std::to_string(kMaxImports) + " peer allocations already";
     ipc::note_cap_refusal(*why);

@@ -60,6 +60,8 @@ class CommInfo(ctypes.Structure):
         ("auto_read", ctypes.c_int), ("peer_link", ctypes.c_int * 16), ("peer_hops", ctypes.c_int * 16),
         ("auto_reason", ctypes.c_char * 160), ("read_grid_calls", ctypes.c_ulonglong),
         ("window_calls", ctypes.c_ulonglong), ("windows", ctypes.c_int), ("auto_grid", ctypes.c_int),
+        # since mncclVersion 501
+        ("retired_imports", ctypes.c_int),
     ]
 
 

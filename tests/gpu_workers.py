@@ -124,9 +124,19 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
             if not inplace:
                 recv.fill_byte(0xAB)
             # "window": send / recv registered (mncclCommRegister, collective: every rank runs the
-            # same cases in the same order) for this case, deregistered after it
-            wins = []
-            if case.get("window"):
+            # same cases in the same order) for this case, deregistered after it.  "window_optional"
+            # (the mixed stress): a registration the library refuses -- on every rank alike, it is
+            # collective -- is recorded and the case runs unregistered (co-located ranks: the GPU
+            # driver can lose a buffer's export handle, profiles/r5_export_reuse.txt)
+            wins, refused = [], 0
+            if case.get("window") and case.get("window_optional"):
+                for b in ([send] if inplace else [send, recv]):
+                    wrc, h = comm.register_rc(b.ptr, nbytes + off)
+                    if wrc != 0:
+                        refused = wrc
+                        break
+                    wins.append(h)
+            elif case.get("window"):
                 wins.append(comm.register(send.ptr, nbytes + off))
                 if not inplace:
                     wins.append(comm.register(recv.ptr, nbytes + off))
@@ -174,7 +184,8 @@ def allreduce_rank(rank, n, port, cases, env, out_q, barrier=None):
                             "window_calls": ci["window_calls"] - win0,
                             "peer_mappings": ci["peer_mappings"], "ipc_open_failures": ci["ipc_open_failures"],
                             "read_map_failures": ci["read_map_failures"], "closed_freed": ci["closed_freed"],
-                            "live_exports": ci["live_exports"]})
+                            "live_exports": ci["live_exports"], "register_refused": refused,
+                            "retired_imports": ci["retired_imports"]})
             for h in wins:
                 comm.deregister(h)
             send.free()

@@ -36,8 +36,8 @@ static int sim_case(int algo, int n, uint64_t count, uint64_t slice, uint64_t mi
     rp.push_back(r[(size_t)i].data());
   }
   uint64_t steps = 0;
-  uint64_t mask = 0;  // 2 bits per call: the schedule of every call
-  for (int c = 0; c < calls; ++c) mask |= (uint64_t)algo << (2 * c);
+  uint64_t mask = 0;  // 3 bits per call: the schedule of every call (tests/sim_api.py codes)
+  for (int c = 0; c < calls; ++c) mask |= (uint64_t)algo << (3 * c);
   const int rc = mnccl_sim_allreduce(mask, sp.data(), rp.data(), n, count, 0, slice, min_slice, channels, slots, calls,
                                      seed, &steps);
   if (rc != 0) return 1;
@@ -53,7 +53,7 @@ static int sim_case(int algo, int n, uint64_t count, uint64_t slice, uint64_t mi
 int main() {
   int fails = 0;
   const uint64_t counts[] = {7, 1000, 4099, 70001};
-  for (int algo : {0, 2, 3})  // ring, read (push form), read (load form)
+  for (int algo : {0, 2, 3, 4})  // ring, read (push form), read (load form), read's grid form
     for (int n = 2; n <= 8; n += 3)
       for (uint64_t c : counts)
         for (int adaptive = 0; adaptive < 2; ++adaptive) {

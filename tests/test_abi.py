@@ -93,7 +93,7 @@ def test_argument_checks_before_device_work(nccl_lib):
     assert L.mncclLocalReduce(fake, fake, fake, 4, M.ncclFloat, M.ncclAvg, None) == M.ncclInternalError
     assert L.mncclLocalReduce(None, fake, fake, 4, M.ncclFloat, M.ncclSum, None) == M.ncclInvalidArgument
     assert L.mncclCommSetAlgo(None, 0) == M.ncclInvalidArgument
-    assert L.mncclVersion() == 500
+    assert L.mncclVersion() == 501
 
 
 def test_info_struct_layout(nccl_lib):

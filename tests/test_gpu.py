@@ -476,6 +476,30 @@ def test_read_schedule_allocation_churn(dev):
         assert all(x["live_exports"] <= 2 for x in res)
 
 
+def test_same_gpu_freed_imports_leave_later_exports_intact(dev):
+    # the round-5 stress's failure, bisected (tools/r5_export_bisect.py, 5 ranks): fresh 20 MiB
+    # buffers that every peer imported, freed by their owners, then new allocations registered as
+    # windows and run.  On one GPU the driver gives an import the exporter's handle; had the peers
+    # unmapped their imports of the freed buffers, that second delete would take the handle of a
+    # buffer allocated since (its export then fails, or names another buffer: wrong results,
+    # profiles/r5_export_alias.txt).  Same-GPU imports are retired instead (csrc/ipcreg.h
+    # close_import): every registration succeeds, every call bit-exact
+    n = 5
+    cases = []
+    for i in range(4):
+        cases += [_case(dtype="i32", count=n << 20, algo=-1, seed=2100 + 3 * i, fresh=True),
+                  _case(dtype="i32", op="max", count=n + i, algo=0, seed=2101 + 3 * i, window=True),
+                  _case(count=4099 + i, algo=2, seed=2102 + 3 * i, window=True, calls=2, vary=True)]
+    out = _run_allreduce(n, cases, timeout=400)
+    for r in range(n):
+        colocated = out[r]["info"]["ranks_on_device"]
+        res = out[r]["results"]
+        assert all(x["window_calls"] >= 1 for x in res if x["case"].get("window") and x["case"]["algo"] == 2), \
+            [x["window_calls"] for x in res]
+        if colocated == n:  # every peer on this GPU: every freed import retired, none unmapped
+            assert res[-1]["retired_imports"] >= res[-1]["closed_freed"] > 0, res[-1]
+
+
 def test_read_schedule_send_recv_in_one_allocation(dev):
     # out of place with send and recv two regions of ONE allocation on every rank: the owner's
     # descriptor datagram carries that allocation once, both mappings come from one import;
