@@ -280,7 +280,7 @@ def release_rank(rank, n, port, env, nbytes, out_q, barrier=None):
                 freed = f1 - f0
             barrier.wait(120)
         out_q.put((rank, {"rc": rc, "destroy": rc_destroy, "last_algo": info["last_algo"], "freed": freed,
-                          "ok": bool((got == n).all())}))
+                          "ok": bool((got == n).all()), "ranks_on_device": info["ranks_on_device"]}))
     except Exception:
         out_q.put((rank, {"error": traceback.format_exc()}))
 

@@ -781,7 +781,10 @@ def test_read_schedule_many_live_buffers(dev):
 def test_destroy_releases_shared_memory(dev):
     # an allocation a read call exported (dma-buf) and the peers imported is released
     # by its owner's hipFree once every communicator is destroyed (destroy closes the imports of
-    # peers no live communicator talks to, and the last one closes the process's exports)
+    # peers no live communicator talks to, and the last one closes the process's exports) -- when
+    # no peer shares the owner's GPU.  A same-GPU peer keeps its import while its process lives
+    # (csrc/ipcreg.h close_import: the driver's shared handle, DESIGN.md Same-GPU handle loss), so
+    # there the memory stays pinned after the free
     n, nbytes = 3, 256 << 20
     port = GW.free_port()
     out = GW.run_ranks(GW.release_rank, n, lambda r: (r, n, port, {"MINI_NCCL_TIMEOUT_MS": "30000"}, nbytes), 300,
@@ -791,7 +794,10 @@ def test_destroy_releases_shared_memory(dev):
         o = out[r]
         assert "error" not in o, o["error"]
         assert o["rc"] == 0 and o["destroy"] == 0 and o["ok"] and o["last_algo"] == 2, o
-        assert o["freed"] >= nbytes * 9 // 10, o  # the memory came back at hipFree
+        if o["ranks_on_device"] == 1:
+            assert o["freed"] >= nbytes * 9 // 10, o  # the memory came back at hipFree
+        else:
+            assert o["freed"] < nbytes // 2, o  # held by the same-GPU peers' imports until they exit
 
 
 def test_count_beyond_int32(dev):
