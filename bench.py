@@ -415,9 +415,13 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_po
 PERF_TEST_MIB = [1, 16, 64, 128]  # tests/perf_test.cpp:69
 
 
-def size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks, warm=5, reps=20):
-    """algbw of this library (default schedule) and of RCCL at the reference perf_test's sizes"""
-    rows = []
+def size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks, warm=5, reps=20, who=("mini_nccl", "rccl"),
+               rows=None):
+    """algbw of this library (default schedule) and of RCCL at the reference perf_test's sizes.
+    who: the columns measured; rows: an earlier call's rows to add them to (bench.py measures its
+    own column right after the schedules, RCCL's among the extras)"""
+    rows = [] if rows is None else rows
+    by_mib = {r["MiB"]: r for r in rows}
     for mib in PERF_TEST_MIB:
         k = (mib << 20) // 4
         if k > send.numel():
@@ -429,10 +433,10 @@ def size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks, 
             if rc != 0:
                 raise M.NcclError(rc, "ncclAllReduce")
 
-        row = {"MiB": mib}
+        row = by_mib.get(mib) or {"MiB": mib}
         for name, fn in (("mini_nccl", ours), ("rccl", None if pg is None else
                                                   (lambda: torch.distributed.all_reduce(r_, group=pg)))):
-            if fn is None:
+            if fn is None or name not in who:
                 continue
             try:
                 for _ in range(warm):
@@ -442,9 +446,11 @@ def size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks, 
                 t0 = time.perf_counter()
                 for _ in range(reps):
                     fn()
+                t1 = time.perf_counter()
                 torch.cuda.synchronize()
                 dt = max_over_ranks(time.perf_counter() - t0) / reps
                 row[name + "_us"] = round(dt * 1e6, 1)
+                row[name + "_host_us"] = round(max_over_ranks(t1 - t0) / reps * 1e6, 1)  # the enqueue loop alone
                 row[name + "_algbw_GBps"] = round(k * 4 / dt / 1e9, 2)
             except Exception as e:
                 if name == "mini_nccl":
@@ -452,12 +458,14 @@ def size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks, 
                 pg = None  # RCCL refused (e.g. two ranks on one GPU): skip it from here on
                 row["rccl_error"] = str(e)[:80]
                 dist.barrier()
-        ok = comm.async_error() == 0
-        ours()
-        torch.cuda.synchronize()
-        row["schedule"] = {0: "ring", 2: "read", 3: "oneshot"}.get(comm.info()["last_algo"], "?")
-        row["ok"] = max_over_ranks(0.0 if (ok and bool((r_ == float(n)).all().item())) else 1.0) == 0.0
-        rows.append(row)
+        if "mini_nccl" in who:
+            ok = comm.async_error() == 0
+            ours()
+            torch.cuda.synchronize()
+            row["schedule"] = {0: "ring", 2: "read", 3: "oneshot"}.get(comm.info()["last_algo"], "?")
+            row["ok"] = max_over_ranks(0.0 if (ok and bool((r_ == float(n)).all().item())) else 1.0) == 0.0
+        if mib not in by_mib:
+            rows.append(row)
     return rows
 
 
@@ -879,8 +887,8 @@ def main():
             # auto: read where the topology rule allows it on every pair of ranks, else the ring
             # (schedule.h topology_blocks_read; the library decides, the line reports)
             args.algo = ("read" if info["auto_read"] else "ring") if info["algo"] < 0 else ALGO_NAMES[info["algo"]]
-            # ... its large calls in the grid form when every rank has a GPU of its own (auto_grid;
-            # schedule.h read_grid_fits: <= 8 ranks, chunks of >= 4 MiB in whole 16-byte vectors)
+            # ... its large calls in the grid form (auto_grid; schedule.h read_grid_form: <= 8 ranks,
+            # chunks of >= 4 MiB in whole 16-byte vectors, the push form)
             chunk_b = (count // n) * esz
             if (args.algo == "read" and info["auto_grid"] and n <= 8 and chunk_b >= (4 << 20)
                     and chunk_b % 16 == 0):
@@ -1021,8 +1029,8 @@ def main():
                         "beside it in schedules.ring with its own roofline and link fractions; headline_check "
                         "states whether this line's own numbers uphold that default"
                         if headline_algo == "read" else
-                        "the library default for device buffers when every rank has a GPU of its own (MINI_NCCL_ALGO="
-                        "auto -> read in its grid form: a one-wave START, a grid of one-batch workgroups that fold each "
+                        "the library default for device buffers (MINI_NCCL_ALGO="
+                        "auto -> read, its large calls in the grid form: a one-wave START, a grid of one-batch workgroups that fold each "
                         "KiB of the rank's chunk from the peers' send buffers in the ring's association order and push "
                         "it into every peer's recv, a one-wave DONE); the persistent read kernel and the north star's "
                         "ring are measured beside it (schedules.read, schedules.ring), headline_check compares them"
@@ -1125,6 +1133,27 @@ def main():
                     "form_holds": dflt["value"] >= other["value"]})
         if rank == 0:
             arm(result)
+        # 3b. this library at the reference perf_test's sizes and small calls by schedule, right
+        # after the schedules (the link probes below left later small calls of co-located ranks
+        # 5x slower on the one-GPU proxy, profiles/r5_bench_size_order.txt); RCCL's column of
+        # `sizes` is added among the extras
+        if args.dtype == "f32":
+            if rank == 0:
+                log("sizes, small calls")
+            try:
+                inject("sizes")
+                result["sizes"] = size_curve(M, torch, dist, comm, None, send, recv, stream, n, max_over_ranks,
+                                             who=("mini_nccl",))
+            except Exception as e:
+                result["sizes"] = {"error": str(e)[:200]}
+            try:
+                inject("small_calls")
+                result["small_calls"] = small_calls(M, torch, dist, comm, send, recv, stream, n, max_over_ranks)
+            except Exception as e:
+                result["small_calls"] = {"error": str(e)[:200]}
+            comm.set_algo(M.ALGO_AUTO if auto_mode else ALGO_IDS[args.algo])
+            if rank == 0:
+                arm(result)
         # 4. the xGMI roofline the schedules are bound by, after the schedules themselves: bytes
         # per link with the hot path's access forms, one link per rank (the ring's) and every link
         # at once (read's loads and pushes)
@@ -1294,27 +1323,16 @@ def main():
             pg = None
         if rank == 0:
             arm(result)
-        # the reference's perf_test sizes (perf_test.cpp:69: 1/16/64/128 MiB), this library's
-        # default schedule next to RCCL's all-reduce, device-resident fp32
-        if rank == 0:
-            log("extras: sizes")
-        try:
-            inject("sizes")
-            if args.dtype == "f32":
-                result["sizes"] = size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks)
-        except Exception as e:
-            result["sizes"] = {"error": str(e)[:200]}
-        if rank == 0:
-            arm(result)
-        # small calls by schedule (the one-shot's place in auto is to be re-decided per topology)
-        if args.dtype == "f32":
+        # the reference's perf_test sizes (perf_test.cpp:69: 1/16/64/128 MiB): RCCL's all-reduce
+        # beside this library's column (measured after the schedules), device-resident fp32
+        if pg is not None and args.dtype == "f32" and isinstance(result.get("sizes"), list):
             if rank == 0:
-                log("extras: small calls")
+                log("extras: RCCL at the perf_test sizes")
             try:
-                inject("small_calls")
-                result["small_calls"] = small_calls(M, torch, dist, comm, send, recv, stream, n, max_over_ranks)
+                size_curve(M, torch, dist, comm, pg, send, recv, stream, n, max_over_ranks, who=("rccl",),
+                           rows=result["sizes"])
             except Exception as e:
-                result["small_calls"] = {"error": str(e)[:200]}
+                result["sizes_rccl_error"] = str(e)[:200]
             if rank == 0:
                 arm(result)
         # the reference's own usage: host buffers in, host buffers out (perf_test.cpp:78-79);

@@ -37,15 +37,17 @@ extern "C" {
    auto_reason, read_grid_calls, window_calls, windows, auto_grid), mncclAlgoReadGrid, registered windows
    (mncclCommRegister / mncclCommDeregister: read calls with no host rendezvous);
    501 imports of a same-GPU peer's memory are never unmapped while the process lives (the GPU
-   driver's handle loss), mncclCommInfo_t grew (same prefix: retired_imports) */
+   driver's handle loss), mncclCommInfo_t grew (same prefix: retired_imports), auto's
+   large read calls take the grid form wherever it fits (co-located ranks too) */
 #define MNCCL_VERSION 501
 
 /* schedules; all produce bit-identical results (same fold order per element) */
 typedef enum {
   mncclAlgoAuto = -1,  /* the library's default: read for device buffers every rank can share
                           when every pair of GPUs is one xGMI hop apart (or shares a GPU: see
-                          mncclCommInfo_t.auto_read) -- its large calls in the grid form when every
-                          rank has a GPU of its own (auto_grid); every other call one-shot when at
+                          mncclCommInfo_t.auto_read) -- its large calls in the grid form (since 501
+                          wherever they fit it, co-located ranks too; 500: only when every rank had
+                          a GPU of its own), the rest persistent; every other call one-shot when at
                           most 64 KiB, else the ring */
   mncclAlgoRing = 0,   /* the reference's ring: neighbour r -> r+1, 2(n-1) steps */
   mncclAlgoDirect = 1, /* removed in 400 (never faster than the ring); mncclCommSetAlgo and
@@ -130,7 +132,8 @@ typedef struct {
   unsigned long long window_calls;       /* calls launched on registered windows: no host rendezvous */
   int windows;                           /* windows registered on this communicator */
   int auto_grid;                         /* 1: auto launches large read calls in the grid form
-                                            (mncclAlgoReadGrid's): every rank has a GPU of its own */
+                                            (mncclAlgoReadGrid's; since 501 whenever auto runs the
+                                            read schedule in its push form) */
   /* since 501 */
   int retired_imports;                   /* process-wide: peers' freed allocations on this GPU still
                                             mapped here (same-GPU ranks only; held until the process

@@ -323,17 +323,10 @@ void Comm::classify_topology(const void* records) {
   }
   const int bad = topology_blocks_read(n, link.data(), hops.data());
   topo_read_ = bad == 0;
-  // every rank alone on its GPU (no pair shares one): auto's large push-form calls take the grid
-  // form -- no residency constraint between co-located persistent kernels to respect, and on the
-  // one-GPU proxy the grid was as fast or faster than the persistent kernel whenever each rank's
-  // kernel had the GPU's dispatcher to itself or shared it with one or three others (2 ranks: 0.684
-  // vs 0.710 ms, 1.21x algbw in the same bench run, placement-immune; 4 ranks equal), slower only
-  // with 8 co-located processes (0.61x) -- a layout a node never has (profiles/r5_proxy_*)
-  alone_ = every_rank_alone(n, link.data());
   char why[160];
   if (bad == 0) {
-    snprintf(why, sizeof why, "read%s: every pair of ranks %s", alone_ ? " (grid form for large calls)" : "",
-             alone_ ? "is one xGMI hop apart" : "shares a GPU or is one xGMI hop apart");
+    snprintf(why, sizeof why, "read (grid form for large calls): every pair of ranks shares a GPU or is one xGMI hop "
+             "apart");
   } else {
     const int q = (bad - 1) / n, p = (bad - 1) % n, l = link[(size_t)bad - 1];
     const char* name = l == kPeerUnknown ? "an unknown link (its GPU is not visible to that process)"
@@ -575,9 +568,8 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   const int nt = cfg_.threads, wg = A / geo_.waves;
   // mncclAlgoReadGrid: the push form's large calls as start / grid fold / done (the same on every
   // rank: the schedule, the push form, vec and the size are rank-uniform)
-  // (auto: when every rank has a GPU of its own, classify_topology's alone_ -- the node)
-  const bool grid = algo == 2 && (algo_ == 4 || (auto_ && alone_)) && cfg_.read_push && vec &&
-                    read_grid_fits(chunk_bytes, n);
+  // (and auto's: schedule.h read_grid_form)
+  const bool grid = algo == 2 && read_grid_form(algo_ == 4, auto_, cfg_.read_push != 0, vec, chunk_bytes, n);
   hipError_t e = grid        ? launch_read_grid(dtype, op, p, stream)
                  : algo == 2 ? launch_read(dtype, op, vec, wg, nt, p, stream)
                  : algo == 3 ? launch_oneshot(dtype, op, vec, wg, nt, p, stream)

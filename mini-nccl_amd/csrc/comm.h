@@ -57,7 +57,7 @@ class Comm {
   // auto's topology rule (schedule.h topology_blocks_read), the same on every rank: whether the
   // default runs the read schedule, why, and how this rank's GPU reaches each peer's
   bool topology_allows_read() const { return topo_read_; }
-  bool auto_grid() const { return auto_ && alone_ && topo_read_; }  // auto's large read calls: grid form
+  bool auto_grid() const { return auto_ && topo_read_ && cfg_.read_push; }  // auto's large read calls: grid form
   const std::string& topology_reason() const { return topo_why_; }
   int peer_link(int q) const { return peer_link_[q]; }
   int peer_hops(int q) const { return peer_hops_[q]; }
@@ -116,7 +116,6 @@ class Comm {
   unsigned long long window_calls_ = 0;     // calls launched on registered windows (no rendezvous)
   int ranks_on_device_ = 1;
   bool topo_read_ = true;        // auto may run the read schedule (every pair: same GPU or 1 xGMI hop)
-  bool alone_ = false;           // every rank has a GPU of its own: auto's large read calls take the grid form
   std::string topo_why_ = "read: one rank";
   int peer_link_[kMaxRanks] = {}, peer_hops_[kMaxRanks] = {};
   uint32_t call_seq_ = 0;        // kernel launches of this communicator (the kernel's start word)

@@ -281,13 +281,16 @@ MNCCL_HD int topology_blocks_read(int n, const int* link, const int* hops) {
   return 0;
 }
 
-// Every rank has a GPU of its own (no pair of ranks shares one): auto then launches its large
-// push-form read calls in the grid form (kernels.hip read_grid_kernel; Comm::classify_topology).
-MNCCL_HD bool every_rank_alone(int n, const int* link) {
-  for (int q = 0; q < n; ++q)
-    for (int p = 0; p < n; ++p)
-      if (p != q && link[q * n + p] == kPeerSameGpu) return false;
-  return true;
+// Whether a read-schedule call launches in the grid form (kernels.hip read_start / read_grid /
+// read_done) rather than the persistent read_kernel: forced (mncclAlgoReadGrid) or under auto,
+// for the push form's calls that fit it.  Auto took the grid only with every rank on a GPU of its
+// own until the grid's workgroup size followed the rank count (read_grid_vectors); since then it
+// measured at least the persistent kernel's rate with co-located ranks too: 2 ranks 1.20x (the
+// persistent kernel's bimodal placement), 4 ranks 1.04x, 8 ranks 0.99-1.02x
+// (profiles/r5_read_vs_grid_forms.txt, r5_bench_n{2,8}_auto_grid.json).  Uniform across ranks:
+// every input is.
+MNCCL_HD bool read_grid_form(bool forced, bool auto_mode, bool push, bool vec, uint64_t chunk_bytes, int n) {
+  return (forced || auto_mode) && push && vec && read_grid_fits(chunk_bytes, n);
 }
 
 // Kernel status bits (host-mapped status word)

@@ -339,9 +339,9 @@ def test_read_grid_parity(dev, n):
              _case(dtype="i32", op="min", count=n * (m + 4) + 1, algo=g, seed=905, expect_grid=True),
              _case(count=n * (m - 256), algo=g, seed=906, expect_grid=False, expect_algo=2),  # below 4 MiB
              _case(dtype="f16", count=n * (2 * m + 1), algo=g, seed=907, expect_grid=False),  # chunk % 16 != 0
-             # auto: the grid form only when every rank has a GPU of its own (schedule.h every_rank_alone)
-             _case(count=n * m + 1, algo=-1, seed=908, expect_algo=2,
-                   expect_grid=len({GW.rank_device(r, NDEV[0]) for r in range(n)}) == n)]
+             # auto: the grid form for the calls it fits, co-located ranks too (schedule.h read_grid_form)
+             _case(count=n * m + 1, algo=-1, seed=908, expect_algo=2, expect_grid=True),
+             _case(count=n * m + 1, algo=2, seed=909, expect_algo=2, expect_grid=False)]  # forced persistent
     _run_allreduce(n, cases, {"GPU_MAX_HW_QUEUES": "2"} if n > 4 else None, timeout=600)
 
 

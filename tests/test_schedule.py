@@ -331,13 +331,21 @@ def test_sim_registered_window_signatures_random_interleavings(sim_lib, n):
 
 
 
-def test_auto_grid_form_only_when_every_rank_has_its_own_gpu(sim_lib):
-    # auto's large read calls take the grid form on a node (one rank per GPU), never when ranks share
-    # a GPU (8 co-located ranks: 0.61x the persistent kernel, profiles/r5_bench_n8_same_gpu.json)
-    assert S.every_rank_alone(_topo(8)[0])
-    assert S.every_rank_alone(_topo(2, kind=S.PCIE)[0])
-    assert not S.every_rank_alone(_topo(8, devices=[0] * 8)[0])
-    assert not S.every_rank_alone(_topo(4, devices=[0, 0, 1, 2])[0])
+def test_read_grid_form_rule(sim_lib):
+    # forced (mncclAlgoReadGrid) or auto: the push form's calls with chunks of >= 4 MiB in whole
+    # 16-byte vectors at 2-8 ranks take the grid form; the load form, unaligned calls, smaller
+    # chunks, more ranks and a forced persistent read (mncclAlgoRead) keep the persistent kernel
+    big = 4 << 20
+    for n in (2, 3, 5, 8):
+        assert S.read_grid_form(True, False, True, True, big, n)
+        assert S.read_grid_form(False, True, True, True, big, n)
+        assert not S.read_grid_form(False, False, True, True, big, n)  # MINI_NCCL_ALGO=read
+        assert not S.read_grid_form(False, True, False, True, big, n)  # MINI_NCCL_READ_PUSH=0
+        assert not S.read_grid_form(False, True, True, False, big, n)  # element-wise path
+        assert not S.read_grid_form(False, True, True, True, big - 16, n)
+        assert not S.read_grid_form(False, True, True, True, big + 8, n)
+    assert not S.read_grid_form(True, True, True, True, big, 9)
+    assert not S.read_grid_form(True, True, True, True, big, 1)
 
 
 
