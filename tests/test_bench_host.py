@@ -119,3 +119,57 @@ def test_verify_order_rejects_another_association(oracle_lib, monkeypatch):
             out.append(y)
         return out
     assert _verify_order_with(monkeypatch, left_fold).startswith("FAILED: element")
+
+
+def test_size_curve_columns_merge_into_one_row_per_size(monkeypatch):
+    # bench.py measures its own column of the perf_test sizes right after the schedules and RCCL's
+    # column among the extras (after the link probes, which slowed later co-located small calls,
+    # profiles/r5_bench_size_order.txt): the second pass adds to the first's rows, one per size
+    import torch
+    import torch.distributed as tdist
+
+    import bench
+
+    n, calls = 2, {"ours": 0, "rccl": 0}
+
+    class _Comm:
+        def all_reduce(self, s, r, k, dt, op, st):
+            calls["ours"] += 1
+            recv[:k] = float(n)
+            return 0
+
+        def async_error(self):
+            return 0
+
+        def info(self):
+            return {"last_algo": 2}
+
+    class _Dist:
+        @staticmethod
+        def barrier():
+            pass
+
+    class _Stream:
+        cuda_stream = 0
+
+    class _M:
+        ncclFloat, ncclSum = 0, 0
+
+        class NcclError(Exception):
+            pass
+
+    def rccl(t, group=None):
+        calls["rccl"] += 1
+
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a: None)
+    monkeypatch.setattr(tdist, "all_reduce", rccl)
+    send, recv = torch.ones(4 << 20), torch.empty(4 << 20)  # 16 MiB: the 1 and 16 MiB points
+    rows = bench.size_curve(_M, torch, _Dist, _Comm(), None, send, recv, _Stream(), n, lambda x: x, who=("mini_nccl",))
+    assert [r["MiB"] for r in rows] == [1, 16] and all(r["ok"] and "mini_nccl_us" in r for r in rows)
+    assert all("rccl_us" not in r for r in rows) and calls["rccl"] == 0
+    ours = calls["ours"]
+    out = bench.size_curve(_M, torch, _Dist, _Comm(), object(), send, recv, _Stream(), n, lambda x: x, who=("rccl",),
+                           rows=rows)
+    assert out is rows and [r["MiB"] for r in rows] == [1, 16]
+    assert all("rccl_us" in r and "mini_nccl_us" in r for r in rows)
+    assert calls["ours"] == ours and calls["rccl"] == 2 * (5 + 20)  # RCCL's pass leaves this library alone
