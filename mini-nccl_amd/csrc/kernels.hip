@@ -1352,8 +1352,11 @@ template <typename T>
 static hipError_t read_grid_for_t(int op, const CollParams& p, hipStream_t st) {
   // V 16-byte vectors per lane per workgroup: V KiB of the chunk each (schedule.h read_grid_vectors)
   const int n = p.n, V = read_grid_vectors(n);
+  // the instantiations below hard-code V per rank count; a rule they do not match is refused
+  // rather than launched with a grid sized for another V
+  if (V != (n <= 4 ? 1 : 2)) return hipErrorInvalidValue;
   const unsigned blocks = (unsigned)((p.chunk_bytes + 1024u * V - 1) / (1024u * V));
-#define GRID_G(OPC, G, V) hipLaunchKernelGGL((read_grid_kernel<T, OPC, G, V>), dim3(blocks), dim3(64), 0, st, p)
+#define GRID_G(OPC, G, VV) hipLaunchKernelGGL((read_grid_kernel<T, OPC, G, VV>), dim3(blocks), dim3(64), 0, st, p)
 #define GRID_CASE(OPC)                    \
   case OPC:                               \
     if (n == 2) GRID_G(OPC, 1, 1);        \
