@@ -190,6 +190,10 @@ SWEEP_POINTS = [
     ("read", {"MINI_NCCL_THREADS": 128}), ("read", {"MINI_NCCL_SYS_FENCE": 1}),
     ("ring", {}), ("ring", {"MINI_NCCL_SLOTS": 4}), ("ring", {"MINI_NCCL_SLICE_SIZE": 524288}),
     ("ring", {"MINI_NCCL_SYS_FENCE": 1}),
+    # the grid form's vectors per lane per workgroup (schedule.h read_grid_vectors: 1 up to 4 ranks,
+    # 2 from 5, decided on the one-GPU proxy): on the node's links, where a remote load waits longer
+    ("read_grid", {}), ("read_grid", {"MINI_NCCL_GRID_VECTORS": 1}), ("read_grid", {"MINI_NCCL_GRID_VECTORS": 2}),
+    ("read_grid", {"MINI_NCCL_GRID_VECTORS": 4}),
 ]
 ALGO_IDS = {"ring": 0, "read": 2, "read_grid": 4}  # mncclAlgo_t
 RAN_AS = {"ring": 0, "read": 2, "read_grid": 2}    # mncclCommInfo_t.last_algo of each (the grid form is read)
@@ -229,7 +233,8 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
     comm = None
     try:
         comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
-        comm.set_algo(ALGO_IDS[algo])
+        comm.set_algo(M.ALGO_AUTO if algo == "auto" else ALGO_IDS[algo])
+        grid0 = comm.info()["read_grid_calls"]
         st = torch.cuda.Stream(device=dev)
         send = torch.ones(count, device=dev, dtype=tdt)
         recv = torch.empty(count, device=dev, dtype=tdt)
@@ -250,10 +255,13 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
         ok = comm.async_error() == 0 and bool((recv == float(n)).all().item())
         ok = ok and verify_calls(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, st, 1, dist.barrier)
         i = comm.info()
-        ok = ok and i["last_algo"] == RAN_AS[algo]  # the point ran its own schedule
+        # the point ran its own schedule (auto: read where the topology allows it, else the ring)
+        want = (2 if i["auto_read"] else 0) if algo == "auto" else RAN_AS[algo]
+        ok = ok and i["last_algo"] == want
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
         return {"GBps": round(count * esz / (dt / reps) / 1e9, 2), "ok": ok, "workgroups": i["channels"],
-                "pipelines": i["pipelines"], "slot_bytes": i["slot_bytes"], "scratch_MiB": i["scratch_bytes"] >> 20}
+                "pipelines": i["pipelines"], "slot_bytes": i["slot_bytes"], "scratch_MiB": i["scratch_bytes"] >> 20,
+                "grid_calls": i["read_grid_calls"] - grid0}
     except Exception as e:
         return {"error": str(e)[:120]}
     finally:
@@ -372,13 +380,14 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_po
     crash still reports what ran.  BASELINE.json's own configs go first (C5, then the C4 grid),
     the exploratory (schedule, knob) points on 256 MiB after them."""
     if with_c4:
-        # BASELINE.json configs[4] (C5): 1 GiB of bf16 / fp16 per rank, library defaults; the
-        # check is exact (integer-valued sums stay exact in 2-byte floats)
+        # BASELINE.json configs[4] (C5): 1 GiB of bf16 / fp16 per rank, library defaults (auto:
+        # read, its large calls in the grid form -- grid_calls says which ran); the check is exact
+        # (integer-valued sums stay exact in 2-byte floats)
         c5 = out["c5_read_1GiB"] = {}
         for dt in ("bf16", "f16"):
             if rank == 0:
-                log(f"C5: read {dt}")
-            c5[dt] = sweep_point(M, torch, dist, dev, n, rank, {}, "read", (1 << 30) // 2, 5, max_over_ranks, dtype=dt)
+                log(f"C5: auto {dt}")
+            c5[dt] = sweep_point(M, torch, dist, dev, n, rank, {}, "auto", (1 << 30) // 2, 5, max_over_ranks, dtype=dt)
             on_point()
         # BASELINE.json configs[3] (C4): ring, 4 GiB fp32, SLICE x WINDOW
         out["c4_buffer_MiB"] = C4_COUNT * 4 >> 20
@@ -387,10 +396,10 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_po
                            "WINDOW x 16, at most 256 pipelines; scratch capped at MINI_NCCL_SCRATCH_MB (512): "
                            "(n-1) x pipelines x 2 x SLICE <= cap, so large slices run fewer pipelines "
                            "(csrc/schedule.h pipeline_geometry; each point reports its geometry)")
-        # the same 4 GiB with the library defaults (the read schedule)
+        # the same 4 GiB with the library defaults (auto: the read schedule, grid form)
         if rank == 0:
-            log("C4: read defaults")
-        out["c4_read_4GiB_defaults"] = sweep_point(M, torch, dist, dev, n, rank, {}, "read", C4_COUNT, 3,
+            log("C4: library defaults")
+        out["c4_read_4GiB_defaults"] = sweep_point(M, torch, dist, dev, n, rank, {}, "auto", C4_COUNT, 3,
                                                    max_over_ranks)
         on_point()
         c4 = out["c4_ring_4GiB"] = []

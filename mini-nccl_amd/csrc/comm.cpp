@@ -570,7 +570,7 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   // rank: the schedule, the push form, vec and the size are rank-uniform)
   // (and auto's: schedule.h read_grid_form)
   const bool grid = algo == 2 && read_grid_form(algo_ == 4, auto_, cfg_.read_push != 0, vec, chunk_bytes, n);
-  hipError_t e = grid        ? launch_read_grid(dtype, op, p, stream)
+  hipError_t e = grid        ? launch_read_grid(dtype, op, p, stream, cfg_.grid_vectors)
                  : algo == 2 ? launch_read(dtype, op, vec, wg, nt, p, stream)
                  : algo == 3 ? launch_oneshot(dtype, op, vec, wg, nt, p, stream)
                              : launch_ring(dtype, op, vec, wg, nt, p, stream);

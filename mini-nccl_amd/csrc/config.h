@@ -21,6 +21,8 @@ struct Config {
   int blocking = 1;                // MINI_NCCL_BLOCKING host waits for the stream (reference behaviour)
   int sys_fence = 0;               // MINI_NCCL_SYS_FENCE 1: system release / acquire fences around each hand-off
   int read_push = 1;               // MINI_NCCL_READ_PUSH read schedule: 1 = each rank pushes its result slices
+  int grid_vectors = 0;            // MINI_NCCL_GRID_VECTORS 1 / 2 / 4: the grid form's 16-byte vectors per lane
+                                   // for fp32 Sum (a tuning knob for the node's sweep); 0 = schedule.h's rule
                                    //   into the peers' recv (default), 0 = the load form (every rank loads
                                    //   the peers' results after a READY per iteration; the comparison form)
   double timeout_ms = 10000.0;     // MINI_NCCL_TIMEOUT_MS (reference watchdog: 10 s)

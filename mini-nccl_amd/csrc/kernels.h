@@ -59,7 +59,8 @@ hipError_t launch_oneshot(int dtype, int op, bool vec, int channels, int threads
                           const CollParams& p, hipStream_t stream);
 // the read schedule's push form for large calls as three launches (start, grid fold, done):
 // schedule.h read_grid_fits(p.chunk_bytes, p.n) (2 <= n <= 8, whole 16-byte vectors), p.go set
-hipError_t launch_read_grid(int dtype, int op, const CollParams& p, hipStream_t stream);
+// vectors: 0 = schedule.h read_grid_vectors; 1 / 2 / 4 (MINI_NCCL_GRID_VECTORS) for fp32 Sum only
+hipError_t launch_read_grid(int dtype, int op, const CollParams& p, hipStream_t stream, int vectors = 0);
 // out[i] = op(local[i], incoming[i]) for i < count
 hipError_t launch_local_reduce(int dtype, int op, void* out, const void* local,
                                const void* incoming, uint64_t count, hipStream_t stream);

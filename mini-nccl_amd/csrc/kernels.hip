@@ -53,6 +53,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "kernels.h"
 #include "schedule.h"
@@ -931,18 +932,20 @@ aborted:
 }
 
 // ---------------------------------------------------------------- read schedule, grid form
-// mncclAlgoReadGrid / MINI_NCCL_ALGO=read_grid (a runtime form, not the default): the push form of
-// a large call (schedule.h read_grid_fits) as three launches on the call's stream --
+// mncclAlgoReadGrid / MINI_NCCL_ALGO=read_grid, and auto's large read calls since 5.1
+// (schedule.h read_grid_form): the push form of a large call (read_grid_fits) as three launches on
+// the call's stream --
 // read_start_kernel (one wave, pipeline 0: START to every peer, wait for theirs, then the device
 // word `go` = this call), read_grid_kernel (the fold with no flag in sight: one one-wave
 // workgroup per 1 KiB of my chunk, dispatched in address order, gone when done) and
 // read_done_kernel (one wave: DONE to every peer, wait for theirs).  Why: the persistent kernel's
 // long-lived waves move a 1:1 read:write stream at 72-80 % of HBM depending on where the buffers
 // landed physically, while the dispatcher's one-batch workgroups held 77-81 % on every placement
-// (tools/mix_probe.hip, profiles/r4_mix_probe_alloc.txt); on the one-GPU proxy it was 1.05x the
-// persistent form at 2 ranks but 0.63x at 8 co-located ranks (profiles/r4_read_grid_ab.txt) --
-// which a node, one rank per GPU, never has -- so the node's bench measures both
-// (schedules.read_grid).  The protocol is the push form's with one pipeline and one iteration
+// (tools/mix_probe.hip, profiles/r4_mix_probe_alloc.txt); on the one-GPU proxy, with the
+// workgroup size following the rank count (read_grid_vectors), 1.16-1.21x the persistent form at
+// 2 / 4 ranks and equal at 3 / 5 / 6 / 8 (profiles/r5_read_vs_grid_forms*.txt,
+// r5_bench_n{2,4,8}_auto_grid.json); the node's bench measures both (schedules.read_grid).  The
+// protocol is the push form's with one pipeline and one iteration
 // (START, DONE: read_msgs_per_call(1) messages on pipeline 0's counters), which the simulator
 // checks for a one-slice read call.  Stream order does the rest: the grid starts after START is
 // through (its workgroups still check `go`: after a failed START they must not touch a peer's
@@ -1349,14 +1352,28 @@ static hipError_t oneshot_for_t(int op, bool vec, int C, int nt, const CollParam
 }
 
 template <typename T>
-static hipError_t read_grid_for_t(int op, const CollParams& p, hipStream_t st) {
+static hipError_t read_grid_for_t(int op, const CollParams& p, hipStream_t st, int vectors) {
   // V 16-byte vectors per lane per workgroup: V KiB of the chunk each (schedule.h read_grid_vectors)
-  const int n = p.n, V = read_grid_vectors(n);
-  // the instantiations below hard-code V per rank count; a rule they do not match is refused
-  // rather than launched with a grid sized for another V
-  if (V != (n <= 4 ? 1 : 2)) return hipErrorInvalidValue;
+  const int n = p.n;
+  // MINI_NCCL_GRID_VECTORS: 1 / 2 / 4 vectors per lane for fp32 Sum (the bench's workload: the
+  // node's sweep weighs them over xGMI); every other call follows the rule
+  const bool tuned = vectors != 0 && std::is_same<T, float>::value && op == kSum;
+  const int V = tuned ? vectors : read_grid_vectors(n);
+  // the rule's instantiations below hard-code V per rank count; a rule they do not match is
+  // refused rather than launched with a grid sized for another V
+  if (!tuned && V != (n <= 4 ? 1 : 2)) return hipErrorInvalidValue;
   const unsigned blocks = (unsigned)((p.chunk_bytes + 1024u * V - 1) / (1024u * V));
 #define GRID_G(OPC, G, VV) hipLaunchKernelGGL((read_grid_kernel<T, OPC, G, VV>), dim3(blocks), dim3(64), 0, st, p)
+  if constexpr (std::is_same<T, float>::value) {
+    if (tuned) {
+#define GRID_V(VV)                                    if (n == 2) GRID_G(kSum, 1, VV);                    else if (n == 3) GRID_G(kSum, 2, VV);               else if (n <= 5) GRID_G(kSum, 4, VV);               else GRID_G(kSum, 7, VV);
+      if (V == 1) { GRID_V(1) }
+      else if (V == 2) { GRID_V(2) }
+      else { GRID_V(4) }
+#undef GRID_V
+      return hipGetLastError();
+    }
+  }
 #define GRID_CASE(OPC)                    \
   case OPC:                               \
     if (n == 2) GRID_G(OPC, 1, 1);        \
@@ -1374,15 +1391,16 @@ static hipError_t read_grid_for_t(int op, const CollParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_read_grid(int dtype, int op, const CollParams& p, hipStream_t st) {
+hipError_t launch_read_grid(int dtype, int op, const CollParams& p, hipStream_t st, int vectors) {
   // the shapes the grid kernel assumes, checked before anything is launched
   if (p.n < 2 || p.n > 8 || p.chunk_bytes % 16 || !p.go || !read_grid_fits(p.chunk_bytes, p.n) ||
-      (p.chunk_bytes + 1023) / 1024 > 0x7fffffffull || (read_grid_vectors(p.n) != 1 && read_grid_vectors(p.n) != 2))
+      (p.chunk_bytes + 1023) / 1024 > 0x7fffffffull || (read_grid_vectors(p.n) != 1 && read_grid_vectors(p.n) != 2) ||
+      (vectors != 0 && vectors != 1 && vectors != 2 && vectors != 4))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(read_start_kernel, dim3(1), dim3(64), 0, st, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-#define M(T) e = read_grid_for_t<T>(op, p, st)
+#define M(T) e = read_grid_for_t<T>(op, p, st, vectors)
   MNCCL_DISPATCH_T(dtype, M)
 #undef M
   if (e != hipSuccess) return e;

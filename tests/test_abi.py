@@ -171,7 +171,14 @@ def test_config_from_env(sim_lib, monkeypatch):
     assert rc == -1 and "no longer" in s
     monkeypatch.setenv("MINI_NCCL_ALGO", "auto")
     rc, s = S.config_describe()
-    assert rc == 0 and "algo=auto" in s
+    assert rc == 0 and "algo=auto" in s and "grid_vectors=0" in s
+    monkeypatch.setenv("MINI_NCCL_GRID_VECTORS", "4")      # the grid form's tuning knob (fp32 Sum)
+    rc, s = S.config_describe()
+    assert rc == 0 and "grid_vectors=4" in s
+    monkeypatch.setenv("MINI_NCCL_GRID_VECTORS", "3")      # not an instantiated width: an init error
+    rc, s = S.config_describe()
+    assert rc == -1 and "GRID_VECTORS" in s
+    monkeypatch.delenv("MINI_NCCL_GRID_VECTORS")
     monkeypatch.setenv("MINI_NCCL_ALGO", "oneshot")      # 4.1
     rc, s = S.config_describe()
     assert rc == 0 and "algo=oneshot" in s

@@ -345,6 +345,22 @@ def test_read_grid_parity(dev, n):
     _run_allreduce(n, cases, {"GPU_MAX_HW_QUEUES": "2"} if n > 4 else None, timeout=600)
 
 
+@pytest.mark.parametrize("n,vectors", [(2, 4), (2, 2), (5, 1), (8, 4)])
+def test_read_grid_vectors_knob(dev, n, vectors):
+    # MINI_NCCL_GRID_VECTORS (the node sweep's tuning knob): fp32 Sum calls in the grid form with
+    # 1 / 2 / 4 vectors per lane per workgroup, tails and in place; other types and ops follow the
+    # rule -- the same bits either way
+    m = 1 << 20
+    cases = [_case(count=n * m + n - 1, algo=4, seed=1900, expect_grid=True),
+             _case(count=n * (m + 256), algo=4, seed=1901, inplace=True, expect_grid=True, calls=2, vary=True),
+             _case(count=n * (3 * m + 64), algo=-1, seed=1902, expect_grid=True),
+             _case(dtype="bf16", op="max", count=n * 2 * m + 3, algo=4, seed=1903, special=True, expect_grid=True)]
+    env = {"MINI_NCCL_GRID_VECTORS": str(vectors)}
+    if n > 4:
+        env["GPU_MAX_HW_QUEUES"] = "2"
+    _run_allreduce(n, cases, env, timeout=600)
+
+
 def test_read_grid_skewed_and_interleaved(dev):
     # grid-form calls between persistent read, ring and one-shot calls on one communicator (the
     # grid form moves pipeline 0's counters only), ranks entering every call out of step
