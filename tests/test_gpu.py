@@ -354,7 +354,7 @@ def test_read_grid_vectors_knob(dev, n, vectors):
     cases = [_case(count=n * m + n - 1, algo=4, seed=1900, expect_grid=True),
              _case(count=n * (m + 256), algo=4, seed=1901, inplace=True, expect_grid=True, calls=2, vary=True),
              _case(count=n * (3 * m + 64), algo=-1, seed=1902, expect_grid=True),
-             _case(dtype="bf16", op="max", count=n * 2 * m + 3, algo=4, seed=1903, special=True, expect_grid=True)]
+             _case(dtype="bf16", op="max", count=n * 2 * m + n - 1, algo=4, seed=1903, special=True, expect_grid=True)]
     env = {"MINI_NCCL_GRID_VECTORS": str(vectors)}
     if n > 4:
         env["GPU_MAX_HW_QUEUES"] = "2"
