@@ -383,6 +383,7 @@ def fullsize_rank(rank, n, port, env, dtype, count, algos, out_q, barrier=None):
         for i, algo in enumerate(algos):
             inplace = i % 2 == 1
             comm.set_algo(algo)
+            grid0 = comm.info()["read_grid_calls"]
             send.upload(x)
             dst = send if inplace else recv
             if not inplace:
@@ -395,8 +396,10 @@ def fullsize_rank(rank, n, port, env, dtype, count, algos, out_q, barrier=None):
             stream.sync()
             secs = time.time() - t0
             got = dst.download(npd, count)
+            ci = comm.info()
             res.append({"algo": algo, "inplace": inplace, "rc": rc, "async": comm.async_error(), "secs": secs,
-                        "last_algo": comm.info()["last_algo"], "digests": block_digests(got)})
+                        "last_algo": ci["last_algo"], "grid_calls": ci["read_grid_calls"] - grid0,
+                        "digests": block_digests(got)})
             del got
         send.free()
         recv.free()

@@ -569,15 +569,19 @@ def _freed_imports(res, n):
 
 
 @pytest.mark.parametrize("dtype,algos,gib,knobs", [
-    ("f32", (2, 0), 1, {}), ("bf16", (2,), 1, {}), ("f16", (2,), 1, {}),
+    # -1: the library default (auto: read, its large calls in the grid form), 2: the persistent
+    # read kernel, 0: the reference's ring
+    ("f32", (-1, 2, 0), 1, {}), ("bf16", (-1, 2), 1, {}), ("f16", (2, -1), 1, {}),
     # C4: 4 GiB fp32, the grid's extreme geometries (WINDOW 16 -> 128 pipelines with 64 KiB
     # slices; 1 MiB slices -> 36 pipelines under the scratch cap), ring as C4 names it
-    ("f32", (0, 2), 4, {"MINI_NCCL_SLICE_SIZE": "65536", "MINI_NCCL_WINDOW_SIZE": "16"}),
+    ("f32", (0, 2, -1), 4, {"MINI_NCCL_SLICE_SIZE": "65536", "MINI_NCCL_WINDOW_SIZE": "16"}),
     ("f32", (0,), 4, {"MINI_NCCL_SLICE_SIZE": "1048576", "MINI_NCCL_WINDOW_SIZE": "64"})],
-    ids=["c3_f32_read_ring", "c5_bf16_read", "c5_f16_read", "c4_64k_w16_ring_read", "c4_1m_w64_ring"])
+    ids=["c3_f32_auto_read_ring", "c5_bf16_auto_read", "c5_f16_read_auto", "c4_64k_w16_ring_read_auto",
+         "c4_1m_w64_ring"])
 def test_allreduce_8_ranks_full_size(dev, dtype, algos, gib, knobs):
-    # BASELINE C3 (8 ranks, 1 GiB fp32; the read default and the reference's ring), C5
-    # (8 ranks, 1 GiB fp16 / bf16) and C4 (8 ranks, 4 GiB fp32) at their FULL sizes, seeded
+    # BASELINE C3 (8 ranks, 1 GiB fp32; the library default in its grid form, the persistent read
+    # kernel and the reference's ring), C5 (8 ranks, 1 GiB fp16 / bf16; default and persistent)
+    # and C4 (8 ranks, 4 GiB fp32) at their FULL sizes, seeded
     # uniform[-1, 1) inputs (order-sensitive), bit-exact against the oracle's closed-form ring
     # fold -- itself pinned to the loop-by-loop restatement of mini_nccl.cu:108-194
     # (tests/test_oracle.py).  The ranks report 16 MiB block digests of their result; the
@@ -599,7 +603,9 @@ def test_allreduce_8_ranks_full_size(dev, dtype, algos, gib, knobs):
         _check_placement(r, n, out[r]["info"], env)
         for res in out[r]["results"]:
             assert res["rc"] == 0 and res["async"] == 0, (r, res["algo"], res["rc"], res["async"])
-            assert res["last_algo"] == res["algo"], (r, res["algo"], res["last_algo"])
+            assert res["last_algo"] == (2 if res["algo"] == -1 else res["algo"]), (r, res["algo"], res["last_algo"])
+            # the default's 1 GiB calls ran in the grid form (chunks of 128 MiB), the forced ones not
+            assert res["grid_calls"] == (1 if res["algo"] == -1 else 0), (r, res["algo"], res["grid_calls"])
             bad = [i for i, (g, e) in enumerate(zip(res["digests"], exp)) if g != e]
             assert len(res["digests"]) == len(exp) and not bad, \
                 f"rank {r} schedule {res['algo']} in_place={res['inplace']}: 16 MiB blocks {bad[:8]} differ"
