@@ -195,6 +195,11 @@ SWEEP_POINTS = [
     ("read_grid", {}), ("read_grid", {"MINI_NCCL_GRID_VECTORS": 1}), ("read_grid", {"MINI_NCCL_GRID_VECTORS": 2}),
     ("read_grid", {"MINI_NCCL_GRID_VECTORS": 4}),
 ]
+# a DDP-bucket-sized call (25 MiB, torch's default bucket): at 8 ranks its chunks are ~3 MiB, just
+# under the grid form's 4 MiB threshold -- the persistent kernel by default, the grid form with
+# MINI_NCCL_GRID_MIN lowered; the node's links decide which is faster for such calls
+MID_POINTS = [("auto", {}), ("auto", {"MINI_NCCL_GRID_MIN": 262144})]
+MID_MIB = 25
 ALGO_IDS = {"ring": 0, "read": 2, "read_grid": 4}  # mncclAlgo_t
 RAN_AS = {"ring": 0, "read": 2, "read_grid": 2}    # mncclCommInfo_t.last_algo of each (the grid form is read)
 ALGO_NAMES = {v: k for k, v in ALGO_IDS.items()}
@@ -417,6 +422,14 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_po
             log(f"sweep {i + 1}/{len(SWEEP_POINTS)}: {algo} {env}")
         r = sweep_point(M, torch, dist, dev, n, rank, env, algo, 64 << 20, 5, max_over_ranks)
         out["points"].append({"algo": algo, "env": {k[len("MINI_NCCL_"):].lower(): v for k, v in env.items()}, **r})
+        on_point()
+    out["mid_points"] = []
+    for algo, env in MID_POINTS:
+        if rank == 0:
+            log(f"sweep {MID_MIB} MiB: {algo} {env}")
+        r = sweep_point(M, torch, dist, dev, n, rank, env, algo, (MID_MIB << 20) // 4, 20, max_over_ranks)
+        out["mid_points"].append({"MiB": MID_MIB, "algo": algo,
+                                  "env": {k[len("MINI_NCCL_"):].lower(): v for k, v in env.items()}, **r})
         on_point()
     return out
 

@@ -94,7 +94,7 @@ void enable_peer_access(int dev, int peer_dev, bool required) {
 // RDMATransport.h:25-48, reduced to what one node over HIP IPC needs).
 struct PeerInfo {
   uint32_t magic;
-  int32_t rank, nranks, pid, device, pad0;
+  int32_t rank, nranks, pid, device, grid_min_kib;  // grid_min_kib: MINI_NCCL_GRID_MIN / 1024
   uint64_t host, nonce, pci;  // nonce: same process <=> same nonce; pci: the physical GPU
   uint64_t slice, scratch_bytes, mbox_bytes, scratch_cap;
   int32_t channels, slots, threads, abi;
@@ -189,6 +189,7 @@ void Comm::exchange_and_map() {
   me.signal_batch = cfg_.signal_batch;
   me.algo = cfg_.algo;
   me.read_push = cfg_.read_push;
+  me.grid_min_kib = (int32_t)(cfg_.grid_min >> 10);
   me.scratch_h = scratch_h_;
   me.mbox_h = mbox_h_;
   me.scratch_ptr = (uint64_t)(uintptr_t)scratch_;
@@ -206,10 +207,10 @@ void Comm::exchange_and_map() {
     // every knob that shapes the kernels' geometry, message protocol or init sequence must agree
     if (p.slice != me.slice || p.channels != me.channels || p.slots != me.slots || p.threads != me.threads ||
         p.window != me.window || p.signal_batch != me.signal_batch || p.scratch_cap != me.scratch_cap ||
-        p.algo != me.algo || p.read_push != me.read_push || p.abi != me.abi)
+        p.algo != me.algo || p.read_push != me.read_push || p.abi != me.abi || p.grid_min_kib != me.grid_min_kib)
       throw std::invalid_argument(
           "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SIGNAL_BATCH / SLOTS / CHANNELS / THREADS / SCRATCH_MB / ALGO / "
-          "READ_PUSH differ between ranks");
+          "READ_PUSH / GRID_MIN differ between ranks");
   }
   ranks_on_device_ = 0;
   for (int q = 0; q < nranks_; ++q)
@@ -569,7 +570,8 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   // mncclAlgoReadGrid: the push form's large calls as start / grid fold / done (the same on every
   // rank: the schedule, the push form, vec and the size are rank-uniform)
   // (and auto's: schedule.h read_grid_form)
-  const bool grid = algo == 2 && read_grid_form(algo_ == 4, auto_, cfg_.read_push != 0, vec, chunk_bytes, n);
+  const bool grid = algo == 2 && read_grid_form(algo_ == 4, auto_, cfg_.read_push != 0, vec, chunk_bytes, n,
+                                                 cfg_.grid_min);
   hipError_t e = grid        ? launch_read_grid(dtype, op, p, stream, cfg_.grid_vectors)
                  : algo == 2 ? launch_read(dtype, op, vec, wg, nt, p, stream)
                  : algo == 3 ? launch_oneshot(dtype, op, vec, wg, nt, p, stream)

@@ -98,6 +98,11 @@ Config Config::from_env() {
   c.sys_fence = env_int("MINI_NCCL_SYS_FENCE", 0) != 0;
   c.read_push = env_int("MINI_NCCL_READ_PUSH", 1) != 0;
   c.grid_vectors = (int)env_int("MINI_NCCL_GRID_VECTORS", 0);
+  const long long gmin = env_int("MINI_NCCL_GRID_MIN", (long long)kReadGridMin);
+  if (gmin < (long long)kReadGridFloor || gmin % 16)
+    throw std::invalid_argument("MINI_NCCL_GRID_MIN=" + std::to_string(gmin) + " (expected a multiple of 16, >= " +
+                                std::to_string(kReadGridFloor) + ")");
+  c.grid_min = (size_t)gmin;
   if (c.grid_vectors != 0 && c.grid_vectors != 1 && c.grid_vectors != 2 && c.grid_vectors != 4)
     throw std::invalid_argument("MINI_NCCL_GRID_VECTORS=" + std::to_string(c.grid_vectors) + " (expected 0, 1, 2 or 4)");
   c.timeout_ms = (double)env_int("MINI_NCCL_TIMEOUT_MS", 10000);
@@ -112,10 +117,10 @@ std::string Config::describe() const {
   char b[320];
   snprintf(b, sizeof b,
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, scratch_cap=%zu MiB, algo=%s, "
-           "blocking=%d, sys_fence=%d, read_push=%d, grid_vectors=%d, timeout=%.0f ms, port=%d",
+           "blocking=%d, sys_fence=%d, read_push=%d, grid_vectors=%d, grid_min=%zu B, timeout=%.0f ms, port=%d",
            slice_size, window_size, signal_batch, slots, channels, threads, scratch_cap >> 20,
            algo < 0 ? "auto" : algo == 2 ? "read" : algo == 3 ? "oneshot" : algo == 4 ? "read_grid" : "ring", blocking,
-           sys_fence, read_push, grid_vectors, timeout_ms, port);
+           sys_fence, read_push, grid_vectors, grid_min, timeout_ms, port);
   return b;
 }
 

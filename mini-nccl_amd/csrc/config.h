@@ -23,6 +23,8 @@ struct Config {
   int read_push = 1;               // MINI_NCCL_READ_PUSH read schedule: 1 = each rank pushes its result slices
   int grid_vectors = 0;            // MINI_NCCL_GRID_VECTORS 1 / 2 / 4: the grid form's 16-byte vectors per lane
                                    // for fp32 Sum (a tuning knob for the node's sweep); 0 = schedule.h's rule
+  size_t grid_min = 4u << 20;      // MINI_NCCL_GRID_MIN: the smallest chunk (bytes) a read call takes the grid
+                                   // form for (schedule.h kReadGridMin; >= 64 KiB, 16-byte multiple; rank-uniform)
                                    //   into the peers' recv (default), 0 = the load form (every rank loads
                                    //   the peers' results after a READY per iteration; the comparison form)
   double timeout_ms = 10000.0;     // MINI_NCCL_TIMEOUT_MS (reference watchdog: 10 s)

@@ -58,7 +58,7 @@ hipError_t launch_read(int dtype, int op, bool vec, int channels, int threads,
 hipError_t launch_oneshot(int dtype, int op, bool vec, int channels, int threads,
                           const CollParams& p, hipStream_t stream);
 // the read schedule's push form for large calls as three launches (start, grid fold, done):
-// schedule.h read_grid_fits(p.chunk_bytes, p.n) (2 <= n <= 8, whole 16-byte vectors), p.go set
+// schedule.h read_grid_fits(p.chunk_bytes, p.n, kReadGridFloor) (2 <= n <= 8, whole 16-byte vectors), p.go set
 // vectors: 0 = schedule.h read_grid_vectors; 1 / 2 / 4 (MINI_NCCL_GRID_VECTORS) for fp32 Sum only
 hipError_t launch_read_grid(int dtype, int op, const CollParams& p, hipStream_t stream, int vectors = 0);
 // out[i] = op(local[i], incoming[i]) for i < count

@@ -1393,7 +1393,7 @@ static hipError_t read_grid_for_t(int op, const CollParams& p, hipStream_t st, i
 
 hipError_t launch_read_grid(int dtype, int op, const CollParams& p, hipStream_t st, int vectors) {
   // the shapes the grid kernel assumes, checked before anything is launched
-  if (p.n < 2 || p.n > 8 || p.chunk_bytes % 16 || !p.go || !read_grid_fits(p.chunk_bytes, p.n) ||
+  if (p.n < 2 || p.n > 8 || p.chunk_bytes % 16 || !p.go || !read_grid_fits(p.chunk_bytes, p.n, kReadGridFloor) ||
       (p.chunk_bytes + 1023) / 1024 > 0x7fffffffull || (read_grid_vectors(p.n) != 1 && read_grid_vectors(p.n) != 2) ||
       (vectors != 0 && vectors != 1 && vectors != 2 && vectors != 4))
     return hipErrorInvalidValue;

@@ -173,12 +173,14 @@ MNCCL_HD bool oneshot_fits(uint64_t chunk_bytes, int n, int C, uint64_t slot_byt
 // The read schedule's grid form (mncclAlgoReadGrid; kernels.hip read_grid_kernel): three launches
 // instead of the persistent kernel -- a one-wave START, a grid of one-batch workgroups that only
 // fold and push, a one-wave DONE -- with the protocol of a one-slice read call on pipeline 0.
-// Chunks of at least kReadGridMin bytes, whole 16-byte vectors, up to 8 ranks (the fold's peer
-// groups); smaller or ragged calls run the persistent read kernel.  Measured in
-// profiles/r4_read_grid_ab.txt.
+// Chunks of at least kReadGridMin bytes (MINI_NCCL_GRID_MIN: a tuning knob, rank-uniform), whole
+// 16-byte vectors, up to 8 ranks (the fold's peer groups); smaller or ragged calls run the
+// persistent read kernel.  Measured in profiles/r4_read_grid_ab.txt and r5_grid_min_ab.txt (on the
+// one-GPU proxy the grid form below 4 MiB chunks was slower or equal).
 constexpr uint64_t kReadGridMin = 4ull << 20;
-MNCCL_HD bool read_grid_fits(uint64_t chunk_bytes, int n) {
-  return n >= 2 && n <= 8 && chunk_bytes >= kReadGridMin && chunk_bytes % 16 == 0;
+constexpr uint64_t kReadGridFloor = 64ull << 10;  // the smallest MINI_NCCL_GRID_MIN
+MNCCL_HD bool read_grid_fits(uint64_t chunk_bytes, int n, uint64_t min_bytes = kReadGridMin) {
+  return n >= 2 && n <= 8 && chunk_bytes >= min_bytes && chunk_bytes % 16 == 0;
 }
 // 16-byte vectors per lane in one grid workgroup (V KiB of the chunk, from every peer): one up to
 // 4 ranks, two from 5 (profiles/r5_grid_v_ab.txt, 1 GiB per rank on the one-GPU proxy: 8 ranks
@@ -289,8 +291,9 @@ MNCCL_HD int topology_blocks_read(int n, const int* link, const int* hops) {
 // persistent kernel's bimodal placement), 4 ranks 1.04x, 8 ranks 0.99-1.02x
 // (profiles/r5_read_vs_grid_forms.txt, r5_bench_n{2,8}_auto_grid.json).  Uniform across ranks:
 // every input is.
-MNCCL_HD bool read_grid_form(bool forced, bool auto_mode, bool push, bool vec, uint64_t chunk_bytes, int n) {
-  return (forced || auto_mode) && push && vec && read_grid_fits(chunk_bytes, n);
+MNCCL_HD bool read_grid_form(bool forced, bool auto_mode, bool push, bool vec, uint64_t chunk_bytes, int n,
+                             uint64_t min_bytes = kReadGridMin) {
+  return (forced || auto_mode) && push && vec && read_grid_fits(chunk_bytes, n, min_bytes);
 }
 
 // Kernel status bits (host-mapped status word)

@@ -300,8 +300,9 @@ int mnccl_call_pipelines(uint64_t nslices, int channels, int waves) { return cal
 
 // schedule.h topology_blocks_read over an n x n matrix (rank q's row: how q's GPU reaches p's)
 int mnccl_topology_blocks_read(int n, const int* link, const int* hops) { return topology_blocks_read(n, link, hops); }
-int mnccl_read_grid_form(int forced, int auto_mode, int push, int vec, uint64_t chunk_bytes, int n) {
-  return read_grid_form(forced != 0, auto_mode != 0, push != 0, vec != 0, chunk_bytes, n) ? 1 : 0;
+int mnccl_read_grid_form(int forced, int auto_mode, int push, int vec, uint64_t chunk_bytes, int n,
+                         uint64_t min_bytes) {
+  return read_grid_form(forced != 0, auto_mode != 0, push != 0, vec != 0, chunk_bytes, n, min_bytes) ? 1 : 0;
 }
 
 // Runs `calls` consecutive all-reduces (send -> recv, fp32; send == recv for in place) on n

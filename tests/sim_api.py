@@ -25,7 +25,7 @@ def load():
         L.mnccl_read_slice.restype = u64
         L.mnccl_call_pipelines.argtypes = [u64, i, i]
         L.mnccl_topology_blocks_read.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(i)]
-        L.mnccl_read_grid_form.argtypes = [i, i, i, i, u64, i]
+        L.mnccl_read_grid_form.argtypes = [i, i, i, i, u64, i, u64]
         L.mnccl_sim_signed_read.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64,
                                             ctypes.POINTER(u64), u64, ctypes.POINTER(i)]
         L.mnccl_oneshot_slice.argtypes = [u64, i, i, u64]
@@ -146,6 +146,8 @@ def signed_read(inputs, sigs, slice_bytes=1024, channels=4, seed=1):
     return recvs, list(mm)
 
 
-def read_grid_form(forced, auto_mode, push, vec, chunk_bytes, n):
-    """csrc/schedule.h read_grid_form: a read-schedule call launches in the grid form."""
-    return bool(load().mnccl_read_grid_form(int(forced), int(auto_mode), int(push), int(vec), chunk_bytes, n))
+def read_grid_form(forced, auto_mode, push, vec, chunk_bytes, n, min_bytes=4 << 20):
+    """csrc/schedule.h read_grid_form: a read-schedule call launches in the grid form (chunks of
+    at least min_bytes: MINI_NCCL_GRID_MIN, default kReadGridMin = 4 MiB)."""
+    return bool(load().mnccl_read_grid_form(int(forced), int(auto_mode), int(push), int(vec), chunk_bytes, n,
+                                            min_bytes))

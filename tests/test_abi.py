@@ -179,6 +179,15 @@ def test_config_from_env(sim_lib, monkeypatch):
     rc, s = S.config_describe()
     assert rc == -1 and "GRID_VECTORS" in s
     monkeypatch.delenv("MINI_NCCL_GRID_VECTORS")
+    rc, s = S.config_describe()
+    assert rc == 0 and f"grid_min={4 << 20} B" in s                # the grid form's threshold (tuning knob)
+    monkeypatch.setenv("MINI_NCCL_GRID_MIN", str(256 << 10))
+    rc, s = S.config_describe()
+    assert rc == 0 and f"grid_min={256 << 10} B" in s
+    monkeypatch.setenv("MINI_NCCL_GRID_MIN", "1000")          # below 64 KiB / not whole vectors: an init error
+    rc, s = S.config_describe()
+    assert rc == -1 and "GRID_MIN" in s
+    monkeypatch.delenv("MINI_NCCL_GRID_MIN")
     monkeypatch.setenv("MINI_NCCL_ALGO", "oneshot")      # 4.1
     rc, s = S.config_describe()
     assert rc == 0 and "algo=oneshot" in s

@@ -361,6 +361,21 @@ def test_read_grid_vectors_knob(dev, n, vectors):
     _run_allreduce(n, cases, env, timeout=600)
 
 
+@pytest.mark.parametrize("n", [2, 8])
+def test_read_grid_min_knob(dev, n):
+    # MINI_NCCL_GRID_MIN lowered to 256 KiB: auto's DDP-bucket-sized calls (25 MiB) and forced grid
+    # calls with chunks from 256 KiB take the grid form, smaller ones the persistent kernel; bit-exact
+    m = (256 << 10) // 4  # 256 KiB of fp32
+    cases = [_case(count=(25 << 20) // 4 + n - 1, algo=-1, seed=2000, expect_grid=True),
+             _case(count=n * m, algo=4, seed=2001, inplace=True, expect_grid=True),
+             _case(count=n * (m - 64), algo=4, seed=2002, expect_grid=False, expect_algo=2),
+             _case(dtype="bf16", op="min", count=n * 2 * m + 1, algo=-1, seed=2003, special=True, expect_grid=True)]
+    env = {"MINI_NCCL_GRID_MIN": str(256 << 10)}
+    if n > 4:
+        env["GPU_MAX_HW_QUEUES"] = "2"
+    _run_allreduce(n, cases, env, timeout=600)
+
+
 def test_read_grid_skewed_and_interleaved(dev):
     # grid-form calls between persistent read, ring and one-shot calls on one communicator (the
     # grid form moves pipeline 0's counters only), ranks entering every call out of step
@@ -737,7 +752,8 @@ def test_single_rank_is_copy_only(dev):
 
 @pytest.mark.parametrize("knob,values", [("MINI_NCCL_SLICE_SIZE", ("131072", "65536")),
                                          ("MINI_NCCL_READ_PUSH", ("1", "0")), ("MINI_NCCL_ALGO", ("ring", "oneshot")),
-                                         ("MINI_NCCL_WINDOW_SIZE", ("64", "16"))])
+                                         ("MINI_NCCL_WINDOW_SIZE", ("64", "16")),
+                                         ("MINI_NCCL_GRID_MIN", (str(4 << 20), str(1 << 20)))])
 def test_mismatched_config_is_system_error(dev, knob, values):
     # every init failure is ncclSystemError, as in the reference (api.cpp:62-65)
     import mini_nccl as M

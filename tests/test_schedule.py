@@ -346,6 +346,9 @@ def test_read_grid_form_rule(sim_lib):
         assert not S.read_grid_form(False, True, True, True, big + 8, n)
     assert not S.read_grid_form(True, True, True, True, big, 9)
     assert not S.read_grid_form(True, True, True, True, big, 1)
+    # MINI_NCCL_GRID_MIN moves the threshold (the node's sweep weighs DDP-bucket-sized calls)
+    assert S.read_grid_form(False, True, True, True, 256 << 10, 8, min_bytes=256 << 10)
+    assert not S.read_grid_form(False, True, True, True, (256 << 10) - 16, 8, min_bytes=256 << 10)
 
 
 
