@@ -61,6 +61,24 @@ def main():
                         comm.link_probe(allp, 0, 10, form=form)
                     comm.link_probe(allp, 0, 10, pull=True)
                     comm.link_probe(allp, 0, 10, pull=True, user=True)
+            elif pre in ("bench3", "bench3v", "bench3o"):
+                # bench.py's three schedules on the 1 GiB buffers: 5 + 20 calls each, then (bench3v)
+                # its integer verify calls and (bench3o) its order-sensitive call too
+                sys.path.insert(0, ROOT)
+                import bench as B
+                for algo in ("ring", "read", "read_grid"):
+                    comm.set_algo({"ring": M.ALGO_RING, "read": M.ALGO_READ, "read_grid": M.ALGO_READ_GRID}[algo])
+                    for _ in range(25):
+                        comm.all_reduce(send.data_ptr(), recv.data_ptr(), 1 << 28, M.ncclFloat, M.ncclSum, st.cuda_stream)
+                    torch.cuda.synchronize()
+                    if pre in ("bench3v", "bench3o"):
+                        B.verify_calls(M, torch, comm, torch.device("cuda", 0), n, rank, send, recv, 1 << 28,
+                                       torch.float32, M.ncclFloat, st, barrier=dist.barrier)
+                    if pre == "bench3o":
+                        B.verify_order(M, torch, comm, torch.device("cuda", 0), n, rank, send, recv, 1 << 28,
+                                       torch.float32, M.ncclFloat, st, dist.barrier)
+                    send.fill_(1.0)
+                comm.set_algo(M.ALGO_AUTO)
             elif pre.startswith("benchprobe"):
                 # bench.py's probe sequence exactly; benchprobe:<i> stops after the i-th variant
                 stop = int(pre.split(":")[1]) if ":" in pre else 99
