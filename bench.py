@@ -380,16 +380,26 @@ def verify_order(M, torch, comm, dev, n, rank, send, recv, count, tdt, ndt, stre
     return "ok"
 
 
-def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_point=lambda: None):
+def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_point=lambda: None, deadline=None):
     """fills `out` point by point (on_point after each), so a guard that ends the run early or a
     crash still reports what ran.  BASELINE.json's own configs go first (C5, then the C4 grid),
-    the exploratory (schedule, knob) points on 256 MiB after them."""
+    the exploratory (schedule, knob) points on 256 MiB after them.  Past `deadline` (time.time())
+    every rank stops before its next point alike (the ranks agree through max_over_ranks)."""
+
+    def go_on():
+        if deadline is None or max_over_ranks(1.0 if time.time() > deadline else 0.0) == 0.0:
+            return True
+        out["stopped"] = "the sweep's time budget ran out: later points skipped (bench.py LINK_RESERVE_S)"
+        return False
+
     if with_c4:
         # BASELINE.json configs[4] (C5): 1 GiB of bf16 / fp16 per rank, library defaults (auto:
         # read, its large calls in the grid form -- grid_calls says which ran); the check is exact
         # (integer-valued sums stay exact in 2-byte floats)
         c5 = out["c5_read_1GiB"] = {}
         for dt in ("bf16", "f16"):
+            if not go_on():
+                return out
             if rank == 0:
                 log(f"C5: auto {dt}")
             c5[dt] = sweep_point(M, torch, dist, dev, n, rank, {}, "auto", (1 << 30) // 2, 5, max_over_ranks, dtype=dt)
@@ -402,6 +412,8 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_po
                            "(n-1) x pipelines x 2 x SLICE <= cap, so large slices run fewer pipelines "
                            "(csrc/schedule.h pipeline_geometry; each point reports its geometry)")
         # the same 4 GiB with the library defaults (auto: the read schedule, grid form)
+        if not go_on():
+            return out
         if rank == 0:
             log("C4: library defaults")
         out["c4_read_4GiB_defaults"] = sweep_point(M, torch, dist, dev, n, rank, {}, "auto", C4_COUNT, 3,
@@ -411,6 +423,8 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_po
         for w in C4_WINDOWS:
             for sl in C4_SLICES:
                 env = {"MINI_NCCL_WINDOW_SIZE": w, "MINI_NCCL_SLICE_SIZE": sl}
+                if not go_on():
+                    return out
                 if rank == 0:
                     log(f"C4: ring {env}")
                 r = sweep_point(M, torch, dist, dev, n, rank, env, "ring", C4_COUNT, 3, max_over_ranks)
@@ -418,6 +432,8 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_po
                 on_point()
     out.update({"buffer": "256 MiB fp32", "points": []})
     for i, (algo, env) in enumerate(SWEEP_POINTS):
+        if not go_on():
+            return out
         if rank == 0:
             log(f"sweep {i + 1}/{len(SWEEP_POINTS)}: {algo} {env}")
         r = sweep_point(M, torch, dist, dev, n, rank, env, algo, 64 << 20, 5, max_over_ranks)
@@ -425,6 +441,8 @@ def run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks, with_c4, out, on_po
         on_point()
     out["mid_points"] = []
     for algo, env in MID_POINTS:
+        if not go_on():
+            return out
         if rank == 0:
             log(f"sweep {MID_MIB} MiB: {algo} {env}")
         r = sweep_point(M, torch, dist, dev, n, rank, env, algo, (MID_MIB << 20) // 4, 20, max_over_ranks)
@@ -694,6 +712,7 @@ def pmc_traffic(key, form=None, fused=None):
 
 
 EXTRAS_LIMIT_S = float(os.environ.get("MNCCL_BENCH_EXTRAS_S", "300"))
+LINK_RESERVE_S = 90.0  # of EXTRAS_LIMIT_S, kept for the link probes that run after the sweeps
 _emitted = []
 
 
@@ -931,7 +950,8 @@ def main():
         def inject(where):
             """MNCCL_BENCH_INJECT=<where>: rehearses the failure paths below (a GPU fault aborts the
             process: the armed line must still come out).  Stages after the ring: run_read (the
-            headline), probe, standalone, rccl, sizes, small_calls, host_buffers, sweep; <stage>_error raises
+            headline), sizes, small_calls, standalone, rccl, host_buffers, sweep, probe (last);
+            <stage>_error raises
             an ncclInternalError there instead; verify_<algo> marks that schedule's results wrong on
             rank 0 (run_algo)"""
             if os.environ.get("MNCCL_BENCH_INJECT") == where and rank == 0:
@@ -1176,63 +1196,68 @@ def main():
             comm.set_algo(M.ALGO_AUTO if auto_mode else ALGO_IDS[args.algo])
             if rank == 0:
                 arm(result)
-        # 4. the xGMI roofline the schedules are bound by, after the schedules themselves: bytes
-        # per link with the hot path's access forms, one link per rank (the ring's) and every link
-        # at once (read's loads and pushes)
-        link = {}
-        try:
-            torch.cuda.synchronize()
-            dist.barrier()
-            inject("probe")
-            # min over ranks (the ceiling is set by the slowest link); max alongside for the spread
-            pn = comm.link_probe(False, 0, 10)
-            pm = comm.link_probe(True, 0, 10)
-            link["probe_next_GBps"] = round(max_over_ranks(-pn) * -1, 2)
-            link["probe_mesh_GBps_per_link"] = round(max_over_ranks(-pm) * -1, 2)
-            link["probe_next_max_GBps"] = round(max_over_ranks(pn), 2)
-            link["probe_mesh_max_GBps_per_link"] = round(max_over_ranks(pm), 2)
-            var = {}
-            # *_user: the peers' ordinary device memory (hipMalloc, what the read schedule loads
-            # from) instead of their uncached scratch
-            for name, form, pull, user in (("push_nt", "nt", False, False), ("push_plain", "plain", False, False),
-                                           ("pull_sys", "sys", True, False), ("pull_plain", "plain", True, False),
-                                           ("pull_sys_user", "sys", True, True), ("push_sys_user", "sys", False, True)):
-                for where, allp in (("next", False), ("mesh", True)):
-                    g = comm.link_probe(allp, 0, 10, form=form, pull=pull, user=user)
-                    var[f"{where}_{name}"] = round(max_over_ranks(-g) * -1, 2)
-            link["probe_variants_GBps_per_link"] = var
-        except Exception as e:
-            link["error"] = str(e)[:200]
-        if rank == 0:
+        def measure_links():
+            """the link probes (step 4), run LAST: after the first probe this process's later calls ran
+            ~100 us slower each on the one-GPU proxy, new communicators included (cause not isolated,
+            profiles/r5_bench_size_order.txt) -- so nothing measured after them, RCCL's number and the
+            sweeps included, may run behind them"""
+            # 4. the xGMI roofline the schedules are bound by, after the schedules themselves: bytes
+            # per link with the hot path's access forms, one link per rank (the ring's) and every link
+            # at once (read's loads and pushes)
+            link = {}
             try:
-                link["topology_rank0"] = peer_topology(local_rank, n, args.same_device)
+                torch.cuda.synchronize()
+                dist.barrier()
+                inject("probe")
+                # min over ranks (the ceiling is set by the slowest link); max alongside for the spread
+                pn = comm.link_probe(False, 0, 10)
+                pm = comm.link_probe(True, 0, 10)
+                link["probe_next_GBps"] = round(max_over_ranks(-pn) * -1, 2)
+                link["probe_mesh_GBps_per_link"] = round(max_over_ranks(-pm) * -1, 2)
+                link["probe_next_max_GBps"] = round(max_over_ranks(pn), 2)
+                link["probe_mesh_max_GBps_per_link"] = round(max_over_ranks(pm), 2)
+                var = {}
+                # *_user: the peers' ordinary device memory (hipMalloc, what the read schedule loads
+                # from) instead of their uncached scratch
+                for name, form, pull, user in (("push_nt", "nt", False, False), ("push_plain", "plain", False, False),
+                                               ("pull_sys", "sys", True, False), ("pull_plain", "plain", True, False),
+                                               ("pull_sys_user", "sys", True, True), ("push_sys_user", "sys", False, True)):
+                    for where, allp in (("next", False), ("mesh", True)):
+                        g = comm.link_probe(allp, 0, 10, form=form, pull=pull, user=user)
+                        var[f"{where}_{name}"] = round(max_over_ranks(-g) * -1, 2)
+                link["probe_variants_GBps_per_link"] = var
             except Exception as e:
-                link["topology_rank0"] = {"error": str(e)[:120]}
-        # each schedule's ceiling from the probed links (min over ranks): the ring moves
-        # 2(n-1)/n of the buffer through one link; read 2/n per link direction, half as loads (its
-        # fold: the probe's mesh pull from user memory) and half as stores (its result pushes: the
-        # mesh push into user memory) -> n / (1/pull + 1/push)
-        if args.same_device:
-            # every "link" of the one-GPU rehearsal is this GPU's HBM, shared with the other ranks'
-            # kernels: a schedule's rate over that is no link fraction (round 2 printed 1.43)
-            link["frac"] = None
-            link["note"] = "ranks share one GPU: the probes measure its HBM, not xGMI; no link fractions"
-        elif "probe_next_GBps" in link:
-            pv = link.get("probe_variants_GBps_per_link", {})
-            pull = pv.get("mesh_pull_sys_user") or pv.get("mesh_pull_sys")
-            push = pv.get("mesh_push_sys_user") or link["probe_mesh_GBps_per_link"]
-            ceil = {"ring": link["probe_next_GBps"] * n / (2 * (n - 1))}
-            if pull and push:
-                ceil["read"] = n / (1.0 / pull + 1.0 / push)
-            link.update({f"{a}_ceiling_GBps": round(c, 2) for a, c in ceil.items()})
-            for a, ptn in result["schedules"].items():
-                if a in ceil and "value" in ptn:
-                    ptn["link_frac"] = round(ptn["value"] / ceil[a], 4)
-            if args.algo in ceil:
-                link["frac"] = round(algbw / ceil[args.algo], 4)
-        result["link"] = link
-        if rank == 0:
-            arm(result)
+                link["error"] = str(e)[:200]
+            if rank == 0:
+                try:
+                    link["topology_rank0"] = peer_topology(local_rank, n, args.same_device)
+                except Exception as e:
+                    link["topology_rank0"] = {"error": str(e)[:120]}
+            # each schedule's ceiling from the probed links (min over ranks): the ring moves
+            # 2(n-1)/n of the buffer through one link; read 2/n per link direction, half as loads (its
+            # fold: the probe's mesh pull from user memory) and half as stores (its result pushes: the
+            # mesh push into user memory) -> n / (1/pull + 1/push)
+            if args.same_device:
+                # every "link" of the one-GPU rehearsal is this GPU's HBM, shared with the other ranks'
+                # kernels: a schedule's rate over that is no link fraction (round 2 printed 1.43)
+                link["frac"] = None
+                link["note"] = "ranks share one GPU: the probes measure its HBM, not xGMI; no link fractions"
+            elif "probe_next_GBps" in link:
+                pv = link.get("probe_variants_GBps_per_link", {})
+                pull = pv.get("mesh_pull_sys_user") or pv.get("mesh_pull_sys")
+                push = pv.get("mesh_push_sys_user") or link["probe_mesh_GBps_per_link"]
+                ceil = {"ring": link["probe_next_GBps"] * n / (2 * (n - 1))}
+                if pull and push:
+                    ceil["read"] = n / (1.0 / pull + 1.0 / push)
+                link.update({f"{a}_ceiling_GBps": round(c, 2) for a, c in ceil.items()})
+                for a, ptn in result["schedules"].items():
+                    if a in ceil and "value" in ptn:
+                        ptn["link_frac"] = round(ptn["value"] / ceil[a], 4)
+                if args.algo in ceil:
+                    link["frac"] = round(algbw / ceil[args.algo], 4)
+            result["link"] = link
+            if rank == 0:
+                arm(result)
         form = kernel_form(args.algo, info["read_push"])
         traffic, tsrc = pmc_traffic(f"{form}_{args.dtype}_1GiB_n{n}" + ("_same_gpu" if args.same_device else ""),
                                     form, fused_bytes(form, esz, count // n, n))
@@ -1315,6 +1340,7 @@ def main():
         guard = threading.Timer(EXTRAS_LIMIT_S, bail)
         guard.daemon = True
         guard.start()
+        t_guard = time.time()
     if n > 1 and not args.no_alt:
         # the comparison ceiling: RCCL's all-reduce on the same buffer (torch.distributed nccl)
         pg = None
@@ -1378,8 +1404,13 @@ def main():
             inject("sweep")
             run_sweeps(M, torch, dist, dev, n, rank, max_over_ranks,
                        with_c4=(n == 8 or os.environ.get("MNCCL_BENCH_C4") == "1"), out=result["sweep"],
-                       on_point=(lambda: arm(result)) if rank == 0 else (lambda: None))
+                       on_point=(lambda: arm(result)) if rank == 0 else (lambda: None),
+                       deadline=t_guard + EXTRAS_LIMIT_S - LINK_RESERVE_S)
             result["sweep"]["wall_s"] = round(time.time() - t_sw, 1)
+    if n > 1:
+        if rank == 0:
+            log("link probes (last)")
+        measure_links()
     if guard is not None:
         guard.cancel()
     if rank == 0:
