@@ -1205,13 +1205,16 @@ def main():
             # per link with the hot path's access forms, one link per rank (the ring's) and every link
             # at once (read's loads and pushes)
             link = {}
+            lc = None
             try:
+                # a communicator of its own (the run's was destroyed before the sweeps), same knobs
+                lc = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
                 torch.cuda.synchronize()
                 dist.barrier()
                 inject("probe")
                 # min over ranks (the ceiling is set by the slowest link); max alongside for the spread
-                pn = comm.link_probe(False, 0, 10)
-                pm = comm.link_probe(True, 0, 10)
+                pn = lc.link_probe(False, 0, 10)
+                pm = lc.link_probe(True, 0, 10)
                 link["probe_next_GBps"] = round(max_over_ranks(-pn) * -1, 2)
                 link["probe_mesh_GBps_per_link"] = round(max_over_ranks(-pm) * -1, 2)
                 link["probe_next_max_GBps"] = round(max_over_ranks(pn), 2)
@@ -1223,11 +1226,14 @@ def main():
                                                ("pull_sys", "sys", True, False), ("pull_plain", "plain", True, False),
                                                ("pull_sys_user", "sys", True, True), ("push_sys_user", "sys", False, True)):
                     for where, allp in (("next", False), ("mesh", True)):
-                        g = comm.link_probe(allp, 0, 10, form=form, pull=pull, user=user)
+                        g = lc.link_probe(allp, 0, 10, form=form, pull=pull, user=user)
                         var[f"{where}_{name}"] = round(max_over_ranks(-g) * -1, 2)
                 link["probe_variants_GBps_per_link"] = var
             except Exception as e:
                 link["error"] = str(e)[:200]
+            finally:
+                if lc is not None:
+                    lc.destroy()
             if rank == 0:
                 try:
                     link["topology_rank0"] = peer_topology(local_rank, n, args.same_device)
