@@ -808,12 +808,14 @@ def main():
         except Exception as e:
             cpu_ring = {"error": str(e)[:200]}
 
-    if args.same_device and n > 4:
+    if args.same_device:
         # rehearsal with every rank on one GPU: each rank's persistent kernel waits for the
         # others', so all n processes' queues must be mapped at once; the GPU's scheduler maps
         # 16 hardware queues across processes at most (8 x 2 ran at full rate, 8 x 4 -- HIP's
         # default, which the GPU box also exports -- time-sliced ~200x slower:
-        # profiles/r2_coloc8_*); set before HIP starts.  Only this rehearsal mode does this.
+        # profiles/r2_coloc8_*), and even 2 processes x 4 time-sliced as soon as one more stream
+        # was created (every later call ~100 us slower; with 2 queues per process no change:
+        # profiles/r5_bench_size_order.txt); set before HIP starts.  Only this rehearsal mode.
         os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MNCCL_BENCH_SAME_DEVICE_QUEUES", "2")
     import torch
     import mini_nccl as M
