@@ -230,11 +230,14 @@ void Comm::exchange_and_map() {
     bool first_here = true;  // warn once per GPU: from its lowest rank
     for (int q = 0; q < rank_; ++q)
       if (all[(size_t)q].pci == me.pci) first_here = false;
-    if (procs.size() > 1 && procs.size() * (size_t)queues > 16 && first_here)
+    // 8 x 4 queues time-sliced every hand-off (profiles/r2_coloc8_*); 2 x 4 did as soon as each
+    // process made one more stream (profiles/r5_bench_size_order.txt), 2 per process never did
+    if (procs.size() > 1 && queues > 2 && first_here)
       fprintf(stderr,
               "[Mini-NCCL] warning: %zu rank processes share GPU %d with up to %d hardware queues each; the "
-              "all-reduce needs every rank's kernel resident at once -- keep processes x GPU_MAX_HW_QUEUES <= 16 "
-              "(and no other process using this GPU), or calls will stall on time-slicing\n",
+              "all-reduce needs every rank's kernel resident at once -- with more than 2 queues per process "
+              "(GPU_MAX_HW_QUEUES) the GPU may time-slice the processes' queues once they hold more streams, "
+              "and every call then stalls; set GPU_MAX_HW_QUEUES=2 (and keep other processes off this GPU)\n",
               procs.size(), device_, queues);
   }
   classify_topology(all.data());
