@@ -173,3 +173,30 @@ def test_size_curve_columns_merge_into_one_row_per_size(monkeypatch):
     assert out is rows and [r["MiB"] for r in rows] == [1, 16]
     assert all("rccl_us" in r and "mini_nccl_us" in r for r in rows)
     assert calls["ours"] == ours and calls["rccl"] == 2 * (5 + 20)  # RCCL's pass leaves this library alone
+
+
+def test_run_sweeps_stops_alike_at_its_budget(monkeypatch):
+    # the sweep keeps LINK_RESERVE_S of the extras' time for the link probes that run after it:
+    # past its deadline every rank stops before its next point (agreed through max_over_ranks)
+    import time
+
+    import bench
+
+    seen = []
+
+    def fake_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_ranks, dtype="f32"):
+        seen.append((algo, dict(env)))
+        return {"GBps": 1.0, "ok": True}
+
+    monkeypatch.setattr(bench, "sweep_point", fake_point)
+    out = bench.run_sweeps(None, None, None, None, 2, 0, lambda x: x, with_c4=False, out={}, deadline=None)
+    assert len(seen) == len(bench.SWEEP_POINTS) + len(bench.MID_POINTS) and "stopped" not in out
+    seen.clear()
+    out = bench.run_sweeps(None, None, None, None, 2, 0, lambda x: x, with_c4=True, out={},
+                           deadline=time.time() - 1)
+    assert seen == [] and "stopped" in out
+    # a peer past its deadline stops this rank too (max over ranks of the flag)
+    seen.clear()
+    out = bench.run_sweeps(None, None, None, None, 2, 0, lambda x: 1.0, with_c4=False, out={},
+                           deadline=time.time() + 3600)
+    assert seen == [] and "stopped" in out
