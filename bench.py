@@ -711,6 +711,22 @@ def pmc_traffic(key, form=None, fused=None):
     return e["hbm_bytes_per_launch"], e.get("source")
 
 
+def trace_of(key, alg_bytes):
+    """The committed kernel trace behind a pmc_summary.json entry (tools/pmc_summary.py writes
+    trace_source / trace_mean_ns / head): kernel_source, the trace's mean launch and the roofline
+    fraction it gives for `alg_bytes` per launch, or {} when there is none."""
+    try:
+        e = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json"))).get(key) or {}
+    except Exception:
+        return {}
+    if not e.get("trace_source") or not e.get("trace_mean_ns"):
+        return {}
+    ms = e["trace_mean_ns"] / 1e6
+    return {"kernel_source": e["trace_source"], "trace_kernel_ms": round(ms, 4),
+            "trace_frac": round(alg_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "trace_head": e.get("head"),
+            "trace_line": e.get("paired_line")}
+
+
 EXTRAS_LIMIT_S = float(os.environ.get("MNCCL_BENCH_EXTRAS_S", "300"))
 LINK_RESERVE_S = 90.0  # of EXTRAS_LIMIT_S, kept for the link probes that run after the sweeps
 _emitted = []
@@ -750,7 +766,8 @@ def arm(result):
 
 
 def emit(result):
-    """write THE one JSON line (at most once) to the real stdout"""
+    """write THE one JSON line (at most once) to the real stdout; `result` is a dict, or a line a
+    rank process already serialised (the self-launch forwards rank 0's)"""
     if not _emitted:
         _emitted.append(True)
         if _crash and _crash[0] is not None:
@@ -758,13 +775,128 @@ def emit(result):
         sys.stdout.flush()
         for attempt in range(5):  # the guard thread may serialise while the main thread adds a point
             try:
-                line = json.dumps(result)
+                line = result if isinstance(result, str) else json.dumps(result)
                 break
             except RuntimeError:
                 time.sleep(0.05)
         else:
             line = json.dumps({k: v for k, v in list(result.items()) if k != "sweep"})
-        os.write(_json_fd[0], (line + "\n").encode())
+        os.write(_json_fd[0], (line.rstrip("\n") + "\n").encode())
+
+
+# ------------------------------------------------------------------ rank processes
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(argv, n, env=None, timeout=None, grace=30.0):
+    """Starts n rank processes of `argv`, one per GPU as the reference's perf_test runs one process
+    per rank (tests/perf_test.cpp:34-49): RANK = LOCAL_RANK = r, WORLD_SIZE = n, MASTER_ADDR
+    127.0.0.1 and a free MASTER_PORT -- the variables torch.distributed.run sets.  The caller must
+    not have touched the GPU (the children are fresh programs, never an exec of this one).  Rank 0's
+    stdout is collected, the other ranks' is dropped (bench.py prints its line from rank 0 only);
+    stderr is shared.  When a rank fails, the rest get `grace` seconds, then SIGTERM (rank 0 then
+    prints its armed line), then SIGKILL; likewise past `timeout`.
+    Returns (exit status: the first rank's to fail, or 0; rank 0's last stdout line or None)."""
+    import subprocess
+    port = free_port()
+    base = dict(os.environ if env is None else env)
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(argv, env=e, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = []
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    t_end = None if timeout is None else time.time() + timeout
+    first_fail, first_rc = None, 0
+    while any(p.poll() is None for p in procs):
+        if first_fail is None and any(p.poll() not in (None, 0) for p in procs):
+            first_fail = time.time()
+            first_rc = next(p.returncode for p in procs if p.returncode not in (None, 0))
+        late = t_end is not None and time.time() > t_end
+        if late or (first_fail is not None and time.time() - first_fail > grace):
+            log(f"rank processes: {'time limit' if late else 'a rank failed'}: ending the rest")
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            t_kill = time.time() + 10
+            while any(p.poll() is None for p in procs) and time.time() < t_kill:
+                time.sleep(0.1)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            for p in procs:
+                p.wait()
+            break
+        time.sleep(0.1)
+    reader.join(10)
+    lines = [ln for ln in (out[0] if out else b"").decode(errors="replace").splitlines() if ln.strip()]
+    rc = first_rc or next((p.returncode for p in procs if p.returncode != 0), 0)
+    return rc, (lines[-1] if lines else None)
+
+
+def launch_plan(gpus, world_env, visible, same_device):
+    """How bench.py runs: "ranks" -- this process is one rank (a launcher set WORLD_SIZE, or one GPU);
+    "spawn" -- start `gpus` rank processes itself (no launcher); ("error", why) -- more GPUs asked for
+    than this process sees and not the one-GPU rehearsal (never a silent co-location or N = 1 run)."""
+    if world_env is not None or gpus <= 1:
+        return "ranks", None
+    if not same_device and gpus > visible:
+        return "error", (f"--gpus {gpus} but {visible} GPU(s) visible: one process per GPU needs {gpus} GPUs "
+                         f"(--same-device rehearses every rank on GPU 0)")
+    return "spawn", None
+
+
+def proxy_allreduce(budget_s=240.0):
+    """VERDICT r5 #4, an extra of the N = 1 run (never `value`): BASELINE.json configs[1]'s shape,
+    2 rank processes on GPU 0 (all ranks on one GPU, as the reference's perf_test, perf_test.cpp:46),
+    256 MiB fp32 per rank, MINI_NCCL_SLICE_SIZE 128 KiB, GPU_MAX_HW_QUEUES=2, 5 warm-up + 20 timed
+    calls (perf_test.cpp:86-99): the library's default schedule and the reference's ring, each
+    checked bit for bit against the ring's association.  Started as fresh rank processes before this
+    process touches the GPU."""
+    t0 = time.time()
+    n, count = 2, 67108864
+    argv = [sys.executable, os.path.abspath(__file__), "--gpus", str(n), "--same-device", "--no-alt", "--no-sweep",
+            "--no-cpu-baseline", "--core-only", "--count", str(count), "--steps", "20", "--warmup", "5"]
+    env = dict(os.environ, MINI_NCCL_SLICE_SIZE="131072", GPU_MAX_HW_QUEUES="2", MNCCL_BENCH_SAME_DEVICE_QUEUES="2")
+    env.pop("MINI_NCCL_ALGO", None)
+    out = {"what": "labelled proxy, never `value`: 2 rank processes sharing GPU 0 (BASELINE.json configs[1]'s size; "
+                   "every 'link' is this GPU's HBM), 256 MiB fp32 per rank, SLICE 128 KiB, GPU_MAX_HW_QUEUES=2, "
+                   "5 + 20 blocking-free calls per schedule, ms and GB/s = max over ranks of the wall clock between "
+                   "barriers; fused_frac_all_ranks = both ranks' fused HBM bytes / rank kernel time / 8 TB/s"}
+    try:
+        rc, line = spawn_ranks(argv, n, env=env, timeout=budget_s)
+        out["rc"] = rc
+        d = json.loads(line) if line else {}
+    except Exception as e:
+        out["error"] = str(e)[:200]
+        return out
+    if "error" in d or not d.get("schedules"):
+        out["error"] = (d.get("error") or "no line from rank 0")[:300]
+    algo = (d.get("config") or {}).get("algo")
+    for name, p in (d.get("schedules") or {}).items():
+        if "value" not in p:
+            out[name] = {"error": p.get("error")}
+            continue
+        rf = p.get("roofline") or {}
+        out["default" if name == algo else name] = {
+            "schedule": name, "GBps": p["value"], "ms_per_call": p["ms_per_step"], "kernel_ms": p.get("kernel_ms"),
+            "sum_frac": rf.get("frac"), "fused_frac": rf.get("fused_frac"),
+            "fused_frac_all_ranks": round(n * rf["fused_frac"], 4) if rf.get("fused_frac") is not None else None,
+            "result_check": p.get("result_check"),
+            "order_sensitive": (p.get("verify") or {}).get("order_sensitive")}
+    out["ok"] = bool(out.get("rc") == 0 and all(
+        isinstance(v, dict) and v.get("result_check") == "ok" and v.get("order_sensitive") == "ok"
+        for k, v in out.items() if k in ("default", "ring")) and "default" in out and "ring" in out)
+    out["wall_s"] = round(time.time() - t0, 1)
+    return out
 
 
 def main():
@@ -783,8 +915,31 @@ def main():
     ap.add_argument("--no-sweep", action="store_true", help="N>1: skip the configuration sweeps")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on GPU 0 (as the reference's perf_test)")
+    ap.add_argument("--core-only", action="store_true",
+                    help="N>1: the schedules and their checks only (the N = 1 run's proxy_allreduce extra)")
     args = ap.parse_args()
     quiet_stdout()
+
+    # no launcher (WORLD_SIZE unset) and --gpus N > 1: this process starts the N rank processes
+    # itself and prints rank 0's line; it never touches the GPU (counting devices does not)
+    plan, why = "ranks", None
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        visible = 0
+        if not args.same_device:
+            import torch
+            visible = torch.cuda.device_count()
+        plan, why = launch_plan(args.gpus, None, visible, args.same_device)
+    if plan == "error":
+        log(why)
+        emit({"metric": METRIC, "value": 0.0, "unit": "GB/s", "n_gpus": args.gpus, "steps": args.steps,
+              "warmup": args.warmup, "higher_is_better": True, "error": why})
+        sys.exit(2)
+    if plan == "spawn":
+        log(f"no launcher: starting {args.gpus} rank processes")
+        rc, line = spawn_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus)
+        emit(line or json.dumps({"metric": METRIC, "value": 0.0, "unit": "GB/s", "n_gpus": args.gpus,
+                                 "higher_is_better": True, "error": f"rank 0 printed no line (exit status {rc})"}))
+        sys.exit(rc)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -800,6 +955,16 @@ def main():
             log("cpu baseline:", json.dumps(cpu))
         except Exception as e:
             log("cpu baseline failed:", e)
+
+    proxy = None
+    if n == 1 and rank == 0 and not args.no_alt and args.dtype == "f32" and args.count == 0:
+        # before this process touches the GPU: the rank processes are fresh programs on GPU 0
+        log("proxy_allreduce: 2 rank processes on GPU 0, 256 MiB fp32")
+        try:
+            proxy = proxy_allreduce()
+        except Exception as e:
+            proxy = {"error": str(e)[:200]}
+        log("proxy_allreduce:", json.dumps(proxy))
 
     cpu_ring = None
     if n > 1 and rank == 0 and not args.no_cpu_baseline:
@@ -1181,7 +1346,7 @@ def main():
         # after the schedules (the link probes below left later small calls of co-located ranks
         # 5x slower on the one-GPU proxy, profiles/r5_bench_size_order.txt); RCCL's column of
         # `sizes` is added among the extras
-        if args.dtype == "f32":
+        if args.dtype == "f32" and not args.core_only:
             if rank == 0:
                 log("sizes, small calls")
             try:
@@ -1281,7 +1446,12 @@ def main():
                               "kernel": kern_key, "kernel_ms": round(ev_ms, 4), "alg_bytes_per_launch": alg_bytes}
         if traffic is not None:
             result["roofline"]["traffic_source"] = tsrc
-    if n > 1:
+        # the committed rocprofv3 kernel trace of the same kernel: its mean launch and
+        # the fraction it gives, beside the live HIP-event figure above
+        tr = trace_of(f"local_reduce_{args.dtype}_1GiB", alg_bytes)
+        if tr:
+            result["roofline"].update(tr)
+    if n > 1 and not args.core_only:
         # roofline.frac above is SURVEY §8(d)'s sum bytes over the FUSED all-reduce kernel's time.
         # For reference only: the same element-wise op as a standalone launch on THIS GPU over the
         # (n-1) * chunk elements a rank reduces per call (same bytes), HIP events around each
@@ -1331,6 +1501,8 @@ def main():
             result["host_inclusive"] = {"error": str(e)[:200]}
     if n == 1:
         result["cpu_baseline"] = cpu
+        if proxy is not None:
+            result["proxy_allreduce"] = proxy
     elif cpu_ring is not None:
         result["cpu_ring_baseline"] = cpu_ring  # the same object as cpu_baseline (kept under its old name)
     if rank == 0:
@@ -1415,7 +1587,7 @@ def main():
                        on_point=(lambda: arm(result)) if rank == 0 else (lambda: None),
                        deadline=t_guard + EXTRAS_LIMIT_S - LINK_RESERVE_S)
             result["sweep"]["wall_s"] = round(time.time() - t_sw, 1)
-    if n > 1:
+    if n > 1 and not args.core_only:
         if rank == 0:
             log("link probes (last)")
         measure_links()

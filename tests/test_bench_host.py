@@ -200,3 +200,54 @@ def test_run_sweeps_stops_alike_at_its_budget(monkeypatch):
     out = bench.run_sweeps(None, None, None, None, 2, 0, lambda x: 1.0, with_c4=False, out={},
                            deadline=time.time() + 3600)
     assert seen == [] and "stopped" in out
+
+
+# ------------------------------------------------------------------ the self-launch
+def test_launch_plan_decisions():
+    import bench
+    assert bench.launch_plan(1, None, 0, False) == ("ranks", None)      # N = 1: this process
+    assert bench.launch_plan(8, "8", 8, False) == ("ranks", None)       # a launcher set WORLD_SIZE
+    assert bench.launch_plan(8, None, 8, False) == ("spawn", None)      # no launcher: 8 rank processes
+    assert bench.launch_plan(2, None, 1, True) == ("spawn", None)       # the one-GPU rehearsal
+    kind, why = bench.launch_plan(8, None, 1, False)                    # never a silent co-location
+    assert kind == "error" and "--gpus 8" in why and "1 GPU(s) visible" in why
+
+
+def test_spawn_ranks_sets_the_launcher_env_and_keeps_rank0_line():
+    sys.path.insert(0, ROOT)
+    import bench
+    child = ("import json, os\n"
+             "if os.environ['RANK'] == '0':\n"
+             "    print('banner before the line')\n"
+             "    print(json.dumps({k: os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR')}))\n"
+             "else:\n"
+             "    print(json.dumps({'rank': os.environ['RANK']}))\n")
+    rc, line = bench.spawn_ranks([sys.executable, "-c", child], 3, timeout=60)
+    assert rc == 0
+    assert json.loads(line) == {"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "3", "MASTER_ADDR": "127.0.0.1"}
+
+
+def test_spawn_ranks_ends_the_rest_when_a_rank_fails():
+    sys.path.insert(0, ROOT)
+    import bench
+    child = ("import os, sys, time\n"
+             "if os.environ['RANK'] == '1':\n"
+             "    sys.exit(3)\n"
+             "time.sleep(120)\n")
+    t0 = __import__("time").time()
+    rc, line = bench.spawn_ranks([sys.executable, "-c", child], 2, timeout=60, grace=1.0)
+    assert rc == 3 and line is None
+    assert __import__("time").time() - t0 < 30
+
+
+def test_bench_gpus_n_without_enough_gpus_prints_one_error_line():
+    # this container has no GPU: `python3 bench.py --gpus 4` (no launcher) must neither co-locate
+    # nor fall back to N = 1 -- one line, value 0, the reason, exit status 2
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], capture_output=True,
+                       text=True, timeout=300, cwd=ROOT, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["value"] == 0.0 and d["n_gpus"] == 4 and "GPU(s) visible" in d["error"]
