@@ -183,8 +183,8 @@ def cpu_ring_baseline(n, budget_s=6.0):
 # own communicator (the knobs are read at ncclCommInitRank, as the reference's Config).
 SWEEP_POINTS = [
     # (algo, knobs over the library defaults: 256 one-wave workgroups, 128 KiB slices, 2 slots,
-    #  no hand-off fences, the read schedule's push form)
-    ("read", {}), ("read", {"MINI_NCCL_READ_PUSH": 0}),  # the push form and its comparison form
+    #  no hand-off fences)
+    ("read", {}),
     ("read", {"MINI_NCCL_SLICE_SIZE": 32768}), ("read", {"MINI_NCCL_SLICE_SIZE": 524288}),
     ("read", {"MINI_NCCL_CHANNELS": 128}), ("read", {"MINI_NCCL_CHANNELS": 512}),
     ("read", {"MINI_NCCL_THREADS": 128}), ("read", {"MINI_NCCL_SYS_FENCE": 1}),
@@ -205,23 +205,20 @@ RAN_AS = {"ring": 0, "read": 2, "read_grid": 2}    # mncclCommInfo_t.last_algo o
 ALGO_NAMES = {v: k for k, v in ALGO_IDS.items()}
 
 
-def kernel_form(algo, read_push=1):
-    """The kernel a schedule launches: ring_kernel, read_kernel in its push / load form (template
-    PUSH), or the push form's grid launches (read_grid_kernel): what a PMC entry must have profiled
-    to describe this line's kernel."""
-    if algo == "read_grid":
-        return "read_grid"
-    return "ring" if algo == "ring" else ("read_push" if read_push else "read_load")
+def kernel_form(algo):
+    """The kernel a schedule launches: ring_kernel, the persistent read_kernel or read's grid
+    launches (read_grid_kernel): what a PMC entry must have profiled to describe this line's kernel
+    ("read_push": the persistent read kernel's key since round 3, when it gained its push form)."""
+    return {"read_grid": "read_grid", "ring": "ring"}.get(algo, "read_push")
 
 
 def fused_bytes(form, esz, chunk, n):
     """Every byte one rank's fused kernel moves through its GPU's HBM per call (DESIGN.md,
     Kernels): the ring reads each chunk of the input and writes each of the output once, and
     2(n-1) chunks land in and are read back from scratch: (6n - 4) chunks; read has no scratch:
-    push form, every chunk of the input read once (n - 1 of them by the peers) and every chunk of
-    the output written once (n - 1 of them by the peers' pushes): 2n; load form, the rank's own
-    result chunk is also read back by the n - 1 peers: 3n - 1."""
-    k = {"ring": 6 * n - 4, "read_push": 2 * n, "read_grid": 2 * n, "read_load": 3 * n - 1}[form]
+    every chunk of the input read once (n - 1 of them by the peers) and every chunk of the output
+    written once (n - 1 of them by the peers' pushes): 2n."""
+    k = {"ring": 6 * n - 4, "read_push": 2 * n, "read_grid": 2 * n}[form]
     return esz * chunk * k
 C4_SLICES = [65536, 131072, 262144, 1048576]
 C4_WINDOWS = [16, 32, 64]
@@ -1088,7 +1085,7 @@ def main():
         comm = M.Comm(n, rank, os.environ.get("MASTER_ADDR", "127.0.0.1"))
         info = comm.info()
         # the headline runs the library's default for device buffers (MINI_NCCL_ALGO=auto: at the
-        # bench's sizes the read schedule in its push form -- one-shot is for calls of <= 64 KiB);
+        # bench's sizes the read schedule -- one-shot is for calls of <= 64 KiB);
         # --algo forces one schedule
         auto_mode = args.algo == "auto"
         if auto_mode:
@@ -1096,7 +1093,7 @@ def main():
             # (schedule.h topology_blocks_read; the library decides, the line reports)
             args.algo = ("read" if info["auto_read"] else "ring") if info["algo"] < 0 else ALGO_NAMES[info["algo"]]
             # ... its large calls in the grid form (auto_grid; schedule.h read_grid_form: <= 8 ranks,
-            # chunks of >= 4 MiB in whole 16-byte vectors, the push form)
+            # chunks of >= 4 MiB in whole 16-byte vectors)
             chunk_b = (count // n) * esz
             if (args.algo == "read" and info["auto_grid"] and n <= 8 and chunk_b >= (4 << 20)
                     and chunk_b % 16 == 0):
@@ -1182,8 +1179,8 @@ def main():
             """one schedule's measured line: algbw, its kernel's roofline fraction (SURVEY s8(d)
             sum bytes over the fused kernel's own time) and every byte it moves through HBM"""
             ms_ = wall / args.steps * 1e3
-            fused = fused_bytes(kernel_form(algo, info["read_push"]), esz, count // n, n)
-            return {"algo": algo, "kernel_form": kernel_form(algo, info["read_push"]),
+            fused = fused_bytes(kernel_form(algo), esz, count // n, n)
+            return {"algo": algo, "kernel_form": kernel_form(algo),
                     "value": round(nbytes / (ms_ / 1e3) / 1e9, 3), "ms_per_step": round(ms_, 4),
                     "kernel_ms": round(ev_ms, 4), "result_check": "ok" if ok else "FAILED",
                     "verify": verifies.get(algo),
@@ -1195,7 +1192,7 @@ def main():
             """the line's headline fields from one schedule's measurement"""
             ms_ = wall / args.steps * 1e3
             bw = nbytes / (ms_ / 1e3) / 1e9
-            fused = fused_bytes(kernel_form(algo, info["read_push"]), esz, count // n, n)
+            fused = fused_bytes(kernel_form(algo), esz, count // n, n)
             fa = fused / (ev_ms / 1e3) / 1e9
             result.update({
                 "value": round(bw, 3),
@@ -1208,7 +1205,7 @@ def main():
                            "pipelines": info["pipelines"], "scratch_bytes": info["scratch_bytes"],
                            "ranks_on_device": info["ranks_on_device"],
                            "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
-                           "read_push": info["read_push"], "headline_schedule": headline_why,
+                           "headline_schedule": headline_why,
                            "auto_schedule": {"read": bool(info["auto_read"]), "reason": info["auto_reason"],
                                              "rank0_peer_link": info["peer_link"],
                                              "rank0_peer_hops": info["peer_hops"],
@@ -1217,7 +1214,7 @@ def main():
                 "roofline": {"bound": "hbm", "achieved": round(sum_bytes / (ev_ms / 1e3) / 1e9, 2),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(sum_bytes / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                             "traffic": None, "kernel": f"{algo}_kernel", "kernel_form": kernel_form(algo, info["read_push"]),
+                             "traffic": None, "kernel": f"{algo}_kernel", "kernel_form": kernel_form(algo),
                              "kernel_ms": round(ev_ms, 4),
                              "alg_bytes_per_launch": sum_bytes, "fused_alg_bytes_per_launch": fused,
                              "fused_achieved": round(fa, 2), "fused_frac": round(fa / HBM_PEAK_GBS, 4)},
@@ -1431,7 +1428,7 @@ def main():
             result["link"] = link
             if rank == 0:
                 arm(result)
-        form = kernel_form(args.algo, info["read_push"])
+        form = kernel_form(args.algo)
         traffic, tsrc = pmc_traffic(f"{form}_{args.dtype}_1GiB_n{n}" + ("_same_gpu" if args.same_device else ""),
                                     form, fused_bytes(form, esz, count // n, n))
         if traffic is not None:

@@ -38,8 +38,12 @@ extern "C" {
    (mncclCommRegister / mncclCommDeregister: read calls with no host rendezvous);
    501 imports of a same-GPU peer's memory are never unmapped while the process lives (the GPU
    driver's handle loss), mncclCommInfo_t grew (same prefix: retired_imports), auto's
-   large read calls take the grid form wherever it fits (co-located ranks too) */
-#define MNCCL_VERSION 501
+   large read calls take the grid form wherever it fits (co-located ranks too);
+   600 the read schedule's load form and MINI_NCCL_READ_PUSH removed (read_push is always 1), a
+   byte budget on retired same-GPU imports (MINI_NCCL_RETIRED_MB; mncclCommInfo_t grew, same
+   prefix: retired_bytes, retired_budget, budget_refusals), window calls carry the launch form in
+   their signature */
+#define MNCCL_VERSION 600
 
 /* schedules; all produce bit-identical results (same fold order per element) */
 typedef enum {
@@ -54,12 +58,10 @@ typedef enum {
                           MINI_NCCL_ALGO reject it */
   mncclAlgoRead = 2    /* no scratch: rank c loads the peers' slices of chunk c straight from
                           their send buffers (mapped per allocation, negotiated per call) and
-                          folds them in the same order.  Push form (the default,
-                          MINI_NCCL_READ_PUSH=1): rank c stores the result into its own recv
-                          AND into every peer's recv -- the peers write chunk c of YOUR recv
-                          during the call, and those writes are visible to your stream's work
-                          after the call.  Load form (MINI_NCCL_READ_PUSH=0): every peer loads
-                          the result from rank c's recv.  A call whose buffers some rank
+                          folds them in the same order, then stores the result into its own
+                          recv AND into every peer's recv -- the peers write chunk c of YOUR
+                          recv during the call, and those writes are visible to your stream's
+                          work after the call.  A call whose buffers some rank
                           cannot share (host memory, a full export table) runs the ring
                           instead, on every rank alike */,
   mncclAlgoOneShot = 3 /* since 401, small calls: every rank stores its whole input into every
@@ -117,7 +119,8 @@ typedef struct {
   unsigned long long liveness_queries;   /* pointer queries this process made to find freed
                                             exports (per call: the call's own buffers + at most
                                             4 others) */
-  int read_push;                         /* MINI_NCCL_READ_PUSH: 1 push form, 0 load form */
+  int read_push;                         /* always 1 since 600 (the load form and MINI_NCCL_READ_PUSH
+                                            were removed); kept for the layout */
   /* since 500 */
   int auto_read;                         /* 1: the topology lets auto run the read schedule (every pair
                                             of ranks shares a GPU or is one xGMI hop apart; the
@@ -138,6 +141,14 @@ typedef struct {
   int retired_imports;                   /* process-wide: peers' freed allocations on this GPU still
                                             mapped here (same-GPU ranks only; held until the process
                                             exits -- DESIGN.md, Same-GPU handle loss) */
+  /* since 600 */
+  unsigned long long retired_bytes;      /* process-wide: bytes those retired imports keep mapped */
+  unsigned long long retired_budget;     /* MINI_NCCL_RETIRED_MB in bytes (default: 1/8 of this GPU's
+                                            memory): once retired_bytes reaches it, a call that would
+                                            map a new buffer of a same-GPU peer runs the ring instead
+                                            (on every rank alike) */
+  unsigned long long budget_refusals;    /* process-wide: same-GPU imports refused by that budget (each
+                                            such call ran the ring; warned once per process) */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,

@@ -185,7 +185,7 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
   info->live_exports = mnccl::ipc::live_exports();
   info->cap_refusals = mnccl::ipc::cap_refusals();
   info->liveness_queries = mnccl::ipc::liveness_queries();
-  info->read_push = k.read_push;
+  info->read_push = 1;  // since 6.0 the read schedule has only its push form
   info->auto_read = c->topology_allows_read() ? 1 : 0;
   for (int q = 0; q < 16; ++q) {
     info->peer_link[q] = q < c->nranks() ? c->peer_link(q) : -1;
@@ -197,6 +197,9 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
   info->windows = (int)c->windows();
   info->auto_grid = c->auto_grid() ? 1 : 0;
   info->retired_imports = (int)mnccl::ipc::retired_imports();
+  info->retired_bytes = mnccl::ipc::retired_bytes();
+  info->retired_budget = mnccl::ipc::retired_budget();
+  info->budget_refusals = mnccl::ipc::budget_refusals();
   memcpy(out, &full, size < sizeof full ? size : sizeof full);
   return ncclSuccess;
 }

@@ -98,10 +98,11 @@ struct PeerInfo {
   uint64_t host, nonce, pci;  // nonce: same process <=> same nonce; pci: the physical GPU
   uint64_t slice, scratch_bytes, mbox_bytes, scratch_cap;
   int32_t channels, slots, threads, abi;
-  int32_t window, signal_batch, algo, read_push;
+  int32_t window, signal_batch, algo, pad0;
   hipIpcMemHandle_t scratch_h, mbox_h;
   uint64_t scratch_ptr, mbox_ptr;  // raw addresses (same-process ranks) / the allocations' bases
   uint64_t scratch_id, mbox_id;    // HIP allocation ids (the import registry's keys)
+  int64_t retired_mb;              // MINI_NCCL_RETIRED_MB as configured (-1: the default)
 };
 constexpr uint32_t kInfoMagic = 0x4d4e4934u;  // 'MNI4' (4.0's record: a 3.x rank fails the check)
 
@@ -184,11 +185,10 @@ void Comm::exchange_and_map() {
   me.channels = cfg_.channels;
   me.slots = cfg_.slots;
   me.threads = cfg_.threads;
-  me.abi = 4;
+  me.abi = 6;  // 6.0: no load form, the retired-import budget in the record
   me.window = cfg_.window_size;
   me.signal_batch = cfg_.signal_batch;
   me.algo = cfg_.algo;
-  me.read_push = cfg_.read_push;
   me.grid_min_kib = (int32_t)(cfg_.grid_min >> 10);
   me.scratch_h = scratch_h_;
   me.mbox_h = mbox_h_;
@@ -196,6 +196,7 @@ void Comm::exchange_and_map() {
   me.mbox_ptr = (uint64_t)(uintptr_t)mbox_;
   me.scratch_id = scratch_id_;
   me.mbox_id = mbox_id_;
+  me.retired_mb = cfg_.retired_mb;
 
   std::vector<PeerInfo> all((size_t)nranks_);
   boot_.allgather(&me, all.data(), sizeof me);
@@ -207,10 +208,11 @@ void Comm::exchange_and_map() {
     // every knob that shapes the kernels' geometry, message protocol or init sequence must agree
     if (p.slice != me.slice || p.channels != me.channels || p.slots != me.slots || p.threads != me.threads ||
         p.window != me.window || p.signal_batch != me.signal_batch || p.scratch_cap != me.scratch_cap ||
-        p.algo != me.algo || p.read_push != me.read_push || p.abi != me.abi || p.grid_min_kib != me.grid_min_kib)
+        p.algo != me.algo || p.abi != me.abi || p.grid_min_kib != me.grid_min_kib ||
+        p.retired_mb != me.retired_mb)
       throw std::invalid_argument(
           "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SIGNAL_BATCH / SLOTS / CHANNELS / THREADS / SCRATCH_MB / ALGO / "
-          "READ_PUSH / GRID_MIN differ between ranks");
+          "GRID_MIN / RETIRED_MB differ between ranks (or their library versions differ)");
   }
   ranks_on_device_ = 0;
   for (int q = 0; q < nranks_; ++q)
@@ -239,6 +241,20 @@ void Comm::exchange_and_map() {
               "(GPU_MAX_HW_QUEUES) the GPU may time-slice the processes' queues once they hold more streams, "
               "and every call then stalls; set GPU_MAX_HW_QUEUES=2 (and keep other processes off this GPU)\n",
               procs.size(), device_, queues);
+  }
+  // the bytes of freed same-GPU peer allocations this process may keep mapped (ipcreg.h
+  // close_import): MINI_NCCL_RETIRED_MB, by default 1/8 of this GPU's memory (36 GB on MI355X)
+  if (ranks_on_device_ > 1) {
+    uint64_t budget = (uint64_t)cfg_.retired_mb << 20;
+    if (cfg_.retired_mb < 0) {
+      size_t fr = 0, total = 0;
+      if (hipMemGetInfo(&fr, &total) != hipSuccess) {
+        (void)hipGetLastError();
+        total = (size_t)288 << 30;
+      }
+      budget = (uint64_t)total / 8;
+    }
+    ipc::set_retired_budget(budget);
   }
   classify_topology(all.data());
   for (int q = 0; q < nranks_; ++q) {
@@ -564,7 +580,6 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.call_seq = seq;
   p.timeout_ticks = (uint64_t)(cfg_.timeout_ms * 1e5);  // s_memrealtime runs at 100 MHz
   p.sys_fence = cfg_.sys_fence;
-  p.read_push = cfg_.read_push;
   p.tail_bytes = tail_bytes;
   p.claim = claim_;
   p.go = go_;
@@ -573,7 +588,7 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   // mncclAlgoReadGrid: the push form's large calls as start / grid fold / done (the same on every
   // rank: the schedule, the push form, vec and the size are rank-uniform)
   // (and auto's: schedule.h read_grid_form)
-  const bool grid = algo == 2 && read_grid_form(algo_ == 4, auto_, cfg_.read_push != 0, vec, chunk_bytes, n,
+  const bool grid = algo == 2 && read_grid_form(algo_ == 4, auto_, vec, chunk_bytes, n,
                                                  cfg_.grid_min);
   hipError_t e = grid        ? launch_read_grid(dtype, op, p, stream, cfg_.grid_vectors)
                  : algo == 2 ? launch_read(dtype, op, vec, wg, nt, p, stream)
@@ -656,9 +671,13 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
         psend[q] = win_s->peer[q] + os;
         precv[q] = win_r->peer[q] + orv;
       }
-      // the call's signature: windows, offsets, count, datatype, op (FNV-1a over the words)
+      // the call's signature: windows, offsets, count, datatype, op and the schedule choice that
+      // picks the kernel form (auto / mncclCommSetAlgo: a grid-form rank paired with a persistent
+      // one could see its DONE met while the peer's other pipelines never start -- ADVICE r5)
+      // (FNV-1a over the words)
       uint64_t sig = 1469598103934665603ull;
-      for (uint64_t v : {win_s->id, os, win_r->id, orv, (uint64_t)count, (uint64_t)dtype, (uint64_t)op, (uint64_t)algo_})
+      const uint64_t mode = auto_ ? ~0ull : (uint64_t)algo_;
+      for (uint64_t v : {win_s->id, os, win_r->id, orv, (uint64_t)count, (uint64_t)dtype, (uint64_t)op, mode})
         for (int b = 0; b < 8; ++b) sig = (sig ^ ((v >> (8 * b)) & 0xff)) * 1099511628211ull;
       sig |= 1;  // never 0 (0 = a negotiated call)
       try {
@@ -723,8 +742,10 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
       try {
         // a peer that does not reach the call within the watchdog's limit fails it, as the
         // kernel's own wait would (the reference's 10 s watchdog, mini_nccl.cu:200-214)
+        // (the schedule choice rides along: ranks that differ in it -- mncclCommSetAlgo is per rank
+        // -- would launch different kernel forms, so they fail the call as a mismatch)
         d = pbuf_.negotiate(send, recv, eligible, count, dtype, op, cfg_.timeout_ms / 1000.0 + 2.0,
-                            [this] { wait_previous_call(); }, psend, precv, &vec_all);
+                            [this] { wait_previous_call(); }, psend, precv, &vec_all, auto_ ? -1 : algo_);
       } catch (const PeerGaveUp& e) {
         return rendezvous_failed(e, true, cur_dev);
       } catch (const std::exception& e) {
@@ -740,8 +761,8 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
         return sticky_;
       }
       if (d == PeerBuffers::kMismatch) {
-        fprintf(stderr, "[Mini-NCCL] rank %d: ranks called ncclAllReduce with different count / datatype / op\n",
-                rank_);
+        fprintf(stderr, "[Mini-NCCL] rank %d: ranks called ncclAllReduce with different count / datatype / op / "
+                "schedule (mncclCommSetAlgo)\n", rank_);
         if (cur_dev != device_) hipSetDevice(cur_dev);
         return ncclInvalidUsage;
       }

@@ -57,7 +57,7 @@ class Comm {
   // auto's topology rule (schedule.h topology_blocks_read), the same on every rank: whether the
   // default runs the read schedule, why, and how this rank's GPU reaches each peer's
   bool topology_allows_read() const { return topo_read_; }
-  bool auto_grid() const { return auto_ && topo_read_ && cfg_.read_push; }  // auto's large read calls: grid form
+  bool auto_grid() const { return auto_ && topo_read_; }  // auto's large read calls: grid form
   const std::string& topology_reason() const { return topo_why_; }
   int peer_link(int q) const { return peer_link_[q]; }
   int peer_hops(int q) const { return peer_hops_[q]; }

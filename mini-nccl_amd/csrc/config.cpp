@@ -33,7 +33,9 @@ void warn_removed_knobs() {
     const char* name;
     const char* now;
   } removed[] = {
-      {"MINI_NCCL_PULL", "removed in 4.0 with the direct schedule; MINI_NCCL_READ_PUSH=0 is the load form of read"},
+      {"MINI_NCCL_PULL", "removed in 4.0 with the direct schedule"},
+      {"MINI_NCCL_READ_PUSH", "removed in 6.0: the read schedule always pushes its results into the peers' recv "
+                              "(the load form was 1.1-1.45x slower wherever it was measured)"},
       {"MINI_NCCL_DIRECT_OVERLAP", "removed in 4.0 with the direct schedule"},
       {"MINI_NCCL_CALIBRATE", "removed in 4.0: auto decides per call (and, since 5.0, from the topology)"},
       {"MINI_NCCL_CALIBRATE_BYTES", "removed in 4.0 with MINI_NCCL_CALIBRATE"},
@@ -96,7 +98,6 @@ Config Config::from_env() {
   }
   c.blocking = env_int("MINI_NCCL_BLOCKING", 1) != 0;
   c.sys_fence = env_int("MINI_NCCL_SYS_FENCE", 0) != 0;
-  c.read_push = env_int("MINI_NCCL_READ_PUSH", 1) != 0;
   c.grid_vectors = (int)env_int("MINI_NCCL_GRID_VECTORS", 0);
   const long long gmin = env_int("MINI_NCCL_GRID_MIN", (long long)kReadGridMin);
   if (gmin < (long long)kReadGridFloor || gmin % 16)
@@ -105,6 +106,8 @@ Config Config::from_env() {
   c.grid_min = (size_t)gmin;
   if (c.grid_vectors != 0 && c.grid_vectors != 1 && c.grid_vectors != 2 && c.grid_vectors != 4)
     throw std::invalid_argument("MINI_NCCL_GRID_VECTORS=" + std::to_string(c.grid_vectors) + " (expected 0, 1, 2 or 4)");
+  c.retired_mb = env_int("MINI_NCCL_RETIRED_MB", -1);
+  if (c.retired_mb < -1) c.retired_mb = -1;
   c.timeout_ms = (double)env_int("MINI_NCCL_TIMEOUT_MS", 10000);
   if (c.timeout_ms < 1) c.timeout_ms = 1;
   c.port = (int)env_int("MINI_NCCL_PORT", 8888);
@@ -117,10 +120,10 @@ std::string Config::describe() const {
   char b[320];
   snprintf(b, sizeof b,
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, scratch_cap=%zu MiB, algo=%s, "
-           "blocking=%d, sys_fence=%d, read_push=%d, grid_vectors=%d, grid_min=%zu B, timeout=%.0f ms, port=%d",
+           "blocking=%d, sys_fence=%d, grid_vectors=%d, grid_min=%zu B, timeout=%.0f ms, port=%d",
            slice_size, window_size, signal_batch, slots, channels, threads, scratch_cap >> 20,
            algo < 0 ? "auto" : algo == 2 ? "read" : algo == 3 ? "oneshot" : algo == 4 ? "read_grid" : "ring", blocking,
-           sys_fence, read_push, grid_vectors, grid_min, timeout_ms, port);
+           sys_fence, grid_vectors, grid_min, timeout_ms, port);
   return b;
 }
 

@@ -20,13 +20,14 @@ struct Config {
   int algo = -1;                   // MINI_NCCL_ALGO    auto (-1) | ring (0) | read (2) | oneshot (3)
   int blocking = 1;                // MINI_NCCL_BLOCKING host waits for the stream (reference behaviour)
   int sys_fence = 0;               // MINI_NCCL_SYS_FENCE 1: system release / acquire fences around each hand-off
-  int read_push = 1;               // MINI_NCCL_READ_PUSH read schedule: 1 = each rank pushes its result slices
   int grid_vectors = 0;            // MINI_NCCL_GRID_VECTORS 1 / 2 / 4: the grid form's 16-byte vectors per lane
                                    // for fp32 Sum (a tuning knob for the node's sweep); 0 = schedule.h's rule
   size_t grid_min = 4u << 20;      // MINI_NCCL_GRID_MIN: the smallest chunk (bytes) a read call takes the grid
                                    // form for (schedule.h kReadGridMin; >= 64 KiB, 16-byte multiple; rank-uniform)
-                                   //   into the peers' recv (default), 0 = the load form (every rank loads
-                                   //   the peers' results after a READY per iteration; the comparison form)
+  long long retired_mb = -1;       // MINI_NCCL_RETIRED_MB: bytes of freed same-GPU peer allocations this process
+                                   // may keep mapped (ipcreg.h close_import), in MiB; -1 = 1/8 of the GPU's
+                                   // memory (Comm resolves it); past it, calls bringing a new same-GPU peer
+                                   // buffer run the ring (rank-uniform)
   double timeout_ms = 10000.0;     // MINI_NCCL_TIMEOUT_MS (reference watchdog: 10 s)
   int port = 8888;                 // MINI_NCCL_PORT   bootstrap port (reference: 8888)
   double bootstrap_timeout_ms = 60000.0;  // MINI_NCCL_BOOTSTRAP_TIMEOUT_MS

@@ -30,7 +30,8 @@ struct Import {
   void* map;      // the dma-buf's mapping (unmapped on close)
   char* local;    // map + the owner's bo_off: the owner's base
   bool same_gpu;  // the owner's memory is on this process's GPU (close_import retires it)
-  bool retired;   // its owner freed it; kept mapped until comm_closed (ipcreg.h close_import)
+  bool retired;   // its owner freed it; kept mapped while the process lives (ipcreg.h close_import)
+  uint64_t bytes; // the mapping's size (the dma-buf's)
 };
 struct BlockImport {
   uint64_t owner, base, id;
@@ -55,6 +56,8 @@ struct State {
   std::vector<std::pair<int, hsa_agent_t>> agents;  // HIP device ordinal -> its HSA agent
   uint64_t open_failures = 0;
   uint64_t liveness_queries = 0, cap_refusals = 0;
+  uint64_t retired_bytes = 0, retired_budget = ~0ull, budget_refusals = 0;
+  bool warned_retired = false, warned_budget = false;
   size_t reap_cursor = 0;                            // next export the round-robin batch checks
   std::vector<std::pair<uint64_t, int>> owner_refs;  // peer process nonce -> live communicators
   int live_comms = 0;
@@ -290,9 +293,11 @@ char* find_import(uint64_t owner, uint64_t base, uint64_t id) {
   return nullptr;
 }
 
-char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shared& d, std::string* why) {
+char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shared& d, std::string* why,
+                  bool* budget_refused) {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
+  if (budget_refused) *budget_refused = false;
   for (const Import& m : s.imports)
     if (!m.retired && m.owner == owner && m.base == base && m.id == id) {
       if (fd >= 0) close(fd);
@@ -308,6 +313,24 @@ char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shar
   hsa_agent_t agent;
   std::string w;
   if (!current_agent(s, &agent, &w)) return fail(w);
+  const uint32_t here = agent_location(agent);
+  const bool same_gpu = here != 0 && here == d.gpu;
+  if (same_gpu && s.retired_bytes >= s.retired_budget) {
+    // one more same-GPU import would pin its memory too once its owner frees it (close_import)
+    close(fd);
+    ++s.budget_refusals;
+    if (budget_refused) *budget_refused = true;
+    char b[256];
+    snprintf(b, sizeof b, "freed allocations of same-GPU peers already hold %llu MiB mapped here (MINI_NCCL_RETIRED_MB "
+             "= %llu)", (unsigned long long)(s.retired_bytes >> 20), (unsigned long long)(s.retired_budget >> 20));
+    *why = b;
+    if (!s.warned_budget) {
+      s.warned_budget = true;
+      fprintf(stderr, "[Mini-NCCL] warning: %s: calls that bring a new buffer of a peer on this GPU run the ring from "
+              "now on (counted in mncclCommInfo_t.budget_refusals)\n", b);
+    }
+    return nullptr;
+  }
   struct stat sb;
   if (fstat(fd, &sb) != 0 || (uint64_t)sb.st_ino != d.ino)
     return fail("the received descriptor does not name the exported dma-buf");
@@ -323,8 +346,7 @@ char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shar
     return nullptr;
   }
   char* local = (char*)p + d.bo_off;
-  const uint32_t here = agent_location(agent);
-  s.imports.push_back(Import{owner, base, id, p, local, here != 0 && here == d.gpu, false});
+  s.imports.push_back(Import{owner, base, id, p, local, same_gpu, false, (uint64_t)sz});
   return local;
 }
 
@@ -333,8 +355,20 @@ bool close_import(uint64_t owner, uint64_t base, uint64_t id) {
   std::lock_guard<std::mutex> g(s.mu);
   for (size_t i = 0; i < s.imports.size(); ++i)
     if (!s.imports[i].retired && s.imports[i].owner == owner && s.imports[i].base == base && s.imports[i].id == id) {
-      if (s.imports[i].same_gpu) {  // see ipcreg.h: unmapped by comm_closed
+      if (s.imports[i].same_gpu) {  // see ipcreg.h: kept mapped while the process lives
         s.imports[i].retired = true;
+        s.retired_bytes += s.imports[i].bytes;
+        const size_t nret = (size_t)std::count_if(s.imports.begin(), s.imports.end(),
+                                                  [](const Import& m) { return m.retired; });
+        if (!s.warned_retired && (nret * 4 >= kMaxImports * 3 ||
+                                  (s.retired_budget != ~0ull && s.retired_bytes * 4 >= s.retired_budget * 3))) {
+          s.warned_retired = true;
+          fprintf(stderr, "[Mini-NCCL] warning: %zu freed allocations of peers on this GPU (%llu MiB) stay mapped in "
+                  "this process (the GPU driver shares their handle, DESIGN.md); at %zu imports or MINI_NCCL_RETIRED_MB "
+                  "= %llu MiB, calls on new peer buffers run the ring -- reuse buffers (a caching allocator) to avoid "
+                  "it\n", nret, (unsigned long long)(s.retired_bytes >> 20), kMaxImports,
+                  (unsigned long long)(s.retired_budget >> 20));
+        }
         return true;
       }
       hsa_amd_interop_unmap_buffer(s.imports[i].map);
@@ -354,6 +388,30 @@ size_t retired_imports() {
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
   return (size_t)std::count_if(s.imports.begin(), s.imports.end(), [](const Import& m) { return m.retired; });
+}
+
+uint64_t retired_bytes() {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  return s.retired_bytes;
+}
+
+void set_retired_budget(uint64_t bytes) {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  s.retired_budget = bytes;
+}
+
+uint64_t retired_budget() {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  return s.retired_budget;
+}
+
+uint64_t budget_refusals() {
+  State& s = st();
+  std::lock_guard<std::mutex> g(s.mu);
+  return s.budget_refusals;
 }
 
 void note_cap_refusal(const std::string& what) {

@@ -61,8 +61,12 @@ size_t live_exports();
 // returned address corresponds to the owner's base.
 char* find_import(uint64_t owner, uint64_t base, uint64_t id);
 // Maps the owner's export from a received duplicate of its descriptor, fd, which this call
-// always closes (a cached import is returned as is); nullptr on failure (*why set).
-char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shared& d, std::string* why);
+// always closes (a cached import is returned as is); nullptr on failure (*why set).  An import of
+// memory of this process's own GPU is refused while the retired imports (close_import) already
+// hold the retired budget's bytes: *budget_refused is then set (not an open failure: the call runs
+// the ring on every rank, as for any mapping that does not happen).
+char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shared& d, std::string* why,
+                  bool* budget_refused = nullptr);
 // Unmaps an import whose owner freed the allocation; the caller makes sure no kernel of this
 // process still reads through it.  False if there was none.  An import of memory of this process's
 // OWN GPU is retired instead -- never found again, kept mapped while the process lives (comm_closed
@@ -70,13 +74,23 @@ char* open_import(uint64_t owner, uint64_t base, uint64_t id, int fd, const Shar
 // handle, so the owner's free and this unmap would delete that handle twice, and a buffer
 // allocated in between loses it -- its later export fails or, worse, names another buffer
 // (profiles/r5_export_alias.txt; DESIGN.md *Same-GPU handle loss*).  The second delete is left to
-// the process's exit.  Retired mappings count against the import cap.
+// the process's exit.  Retired mappings count against the import cap (kMaxImports) and their bytes
+// against the retired budget (set_retired_budget): a co-located job whose peers keep freeing
+// buffers the read schedule shared would otherwise pin that memory without bound.  A one-time
+// warning comes at 3/4 of either bound.
 bool close_import(uint64_t owner, uint64_t base, uint64_t id);
 size_t imports();          // live imports
 size_t retired_imports();  // same-GPU imports of freed allocations, held until the process exits
+uint64_t retired_bytes();  // the bytes those keep mapped
+// The retired budget (bytes; process-wide, the last communicator created sets it: Comm resolves
+// MINI_NCCL_RETIRED_MB, by default 1/8 of the GPU's memory), and the same-GPU imports it refused.
+void set_retired_budget(uint64_t bytes);
+uint64_t retired_budget();
+uint64_t budget_refusals();
 uint64_t open_failures();  // user-buffer imports that failed in this process
-// Exports (kMaxExports, 512) and imports (peerbuf.cpp kMaxImports, 1024) are capped per process;
-// a refused one sends its call to the ring.  Counted here, warned about once per process.
+// Exports (kMaxExports, 512) and imports (kMaxImports, live + retired) are capped per process; a
+// refused one sends its call to the ring.  Counted here, warned about once per process.
+constexpr size_t kMaxImports = 1024;
 void note_cap_refusal(const std::string& what);
 uint64_t cap_refusals();
 

@@ -31,7 +31,6 @@ struct CollParams {
   uint32_t call_seq;       // this launch's sequence number (Comm::wait_for's deadline starts here)
   uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
   int32_t sys_fence;       // system-scope release fence before each ready flag
-  int32_t read_push;       // read schedule: 1 push form, 0 load form (MINI_NCCL_READ_PUSH)
   int32_t pipes;           // the communicator's pipelines (mailbox / scratch / counter layout);
                            // a call's grid may run fewer (schedule.h call_pipelines)
   const char* peer_send[16];  // read schedule: every rank's send buffer, mapped here (own at [rank])

@@ -329,8 +329,12 @@ __device__ __noinline__ bool sig_differs(u64* word, u64 sig) {
   return bad;
 }
 
-// after every peer's START: false (status claimed, nothing touched) if some peer's signature differs
-__device__ __forceinline__ bool starts_agree(const CollParams& p, const Ctl& c, int C, int lane, int w) {
+// after every peer's START: false (status claimed, nothing touched) if some peer's signature differs.
+// *seen: kStatusMismatch when this wave saw the difference itself -- its ABORT word then carries
+// that cause even if another wave won the claim and its status store has not landed yet (ADVICE
+// r5: re-reading the shared status could send a bare abort, and the peer report ncclRemoteError)
+__device__ __forceinline__ bool starts_agree(const CollParams& p, const Ctl& c, int C, int lane, int w,
+                                             uint32_t* seen) {
   if (!p.sig) return true;
   const int n = p.n, r = p.rank;
   const bool peer = lane < n && lane != r;
@@ -339,6 +343,7 @@ __device__ __forceinline__ bool starts_agree(const CollParams& p, const Ctl& c, 
   bool bad = false;
   if (peer) bad = sig_differs(word, p.sig);
   if (__builtin_amdgcn_ballot_w64(bad) == 0) return true;
+  *seen = kStatusMismatch;
   if (lane == 0 && claim_first(c)) st_sys32(c.status, kStatusMismatch);
   return false;
 }
@@ -429,9 +434,10 @@ __device__ __forceinline__ void move(const char* lsrc, char* ldst, rsrc_t in, rs
 }
 
 // the ABORT word a giving-up rank writes into its peers' mailboxes: its rank + 1 (never 0) and
-// its own status (why it gave up) -- the peers report both (Comm::check_status)
-__device__ __forceinline__ u64 abort_word(const CollParams& p) {
-  return ((u64)ld_sys32(p.status) << 32) | (u64)(p.rank + 1);
+// its own status (why it gave up), plus the cause this wave saw itself (`seen`) -- the peers
+// report both (Comm::check_status)
+__device__ __forceinline__ u64 abort_word(const CollParams& p, uint32_t seen = 0) {
+  return ((u64)(ld_sys32(p.status) | seen) << 32) | (u64)(p.rank + 1);
 }
 
 __device__ __forceinline__ void abort_peers(const CollParams& p, int C, int a, int b) {
@@ -550,9 +556,9 @@ constexpr int kMaxWaves = kMaxThreads / 64;
 // MINI_NCCL_ALGO=read (schedule.h): no scratch.  Comm maps every peer's send and recv buffers
 // (dma-buf imports, negotiated per call); rank r folds slice s of its own chunk r straight from
 // the peers' send buffers (sc0 sc1 loads over the links, in ring order) and stores the result
-// into its own recv and (push form, the default) into every peer's recv with sc0 sc1 stores; the
-// load form (MINI_NCCL_READ_PUSH=0, template PUSH = false) instead raises READY and copies every
-// peer's result slice out of that peer's recv.
+// into its own recv and into every peer's recv with sc0 sc1 stores (the push form; 4.0-5.x also
+// built a load form, every peer copying the result out of the owner's recv after a READY: 1.1-1.45x
+// slower everywhere it was measured, removed in 6.0).
 //
 // Fold of slice `nbytes` at byte `coff` of chunk r: acc = op(x_q, acc) in ring order.
 template <typename T, int OPC>
@@ -572,18 +578,14 @@ __device__ __forceinline__ void read_fold_scalar(const CollParams& p, uint64_t c
   }
 }
 
-// Vectors per lane per batch of the read kernel: 16 in the fold (two peers' 16 KiB in flight
-// per wave) and 32 in the copies (32 KiB per wave).  Latency insurance for loads that cross
-// xGMI: a wave's rate is its bytes in flight over the load's round trip, so twice the scratch
-// kernels' batches halve the pipelines a link needs to stay busy; measured free on the one-GPU
-// proxy (2 / 4 / 8 ranks, profiles/r2_read_batch_variants.txt), no VGPR spill (217 VGPRs).
+// Vectors per lane per batch of the read kernel's fold past 8 ranks: 16 (two peers' 16 KiB in
+// flight per wave).  Latency insurance for loads that cross xGMI: a wave's rate is its bytes in
+// flight over the load's round trip, so twice the scratch kernels' batches halve the pipelines a
+// link needs to stay busy; measured free on the one-GPU proxy (profiles/r2_read_batch_variants.txt).
 #ifndef MNCCL_READ_FOLD_U
 #define MNCCL_READ_FOLD_U 16
 #endif
-#ifndef MNCCL_READ_COPY_U
-#define MNCCL_READ_COPY_U 32
-#endif
-constexpr int kReadFoldU = MNCCL_READ_FOLD_U, kReadCopyU = MNCCL_READ_COPY_U;
+constexpr int kReadFoldU = MNCCL_READ_FOLD_U;
 
 // Short slices (below one full batch, and the part of a slice past its full batches): every
 // peer's vectors of a step are loaded at once -- (n-1) x kWideV KiB in flight per wave -- so a
@@ -626,34 +628,6 @@ __device__ __forceinline__ void read_fold_wide(const CollParams& p, uint64_t cof
   }
 }
 
-// vectors [vlo, nvec) of every peer's result slice at byte soff of its chunk, into my recv
-__device__ __forceinline__ void read_copy_wide(const CollParams& p, uint64_t soff, uint32_t vlo, uint32_t nvec,
-                                               int lane) {
-  const int n = p.n, r = p.rank;
-  const uint32_t vb = nvec * 16;
-  for (uint32_t b = vlo; b < nvec; b += 64 * kWideV) {
-    for (int k0 = 1; k0 < n; k0 += kWideG) {
-      v4u y[kWideG][kWideV];
-#pragma unroll
-      for (int g = 0; g < kWideG; ++g)
-        if (k0 + g < n) {
-          const int q = direct_peer(n, r, k0 + g);
-          const rsrc_t in = make_rsrc(p.peer_recv[q] + (u64)q * p.chunk_bytes + soff, vb);
-#pragma unroll
-          for (int u = 0; u < kWideV; ++u) y[g][u] = ld_slot16(in, (b + (uint32_t)(u * 64 + lane)) * 16);
-        }
-#pragma unroll
-      for (int g = 0; g < kWideG; ++g)
-        if (k0 + g < n) {
-          const int q = direct_peer(n, r, k0 + g);
-          const rsrc_t dst = make_rsrc(p.recv + (u64)q * p.chunk_bytes + soff, vb);
-#pragma unroll
-          for (int u = 0; u < kWideV; ++u) st_nt16(dst, (b + (uint32_t)(u * 64 + lane)) * 16, y[g][u]);
-        }
-    }
-  }
-}
-
 // The fold of a slice from 4 to 8 ranks (a node): each batch loads V vectors per lane from EVERY
 // peer at once, and the next batch's loads leave before this batch is folded (two register
 // sets).  The fold's order is fixed (ring order), its load order is not: loaded one peer after
@@ -670,20 +644,17 @@ __device__ __forceinline__ void read_copy_wide(const CollParams& p, uint64_t sof
 #ifndef MNCCL_FOLD_ALL_MIN_N
 #define MNCCL_FOLD_ALL_MIN_N 2
 #endif
-// The read schedule's second half (PUSH, MINI_NCCL_READ_PUSH=1, the default): each rank pushes its result
-// slices into every peer's recv (sc0 sc1 stores, straight from the fold's registers) instead of
-// every rank loading them from the owners' recv after a READY -- no per-iteration READY, no copy
-// phase, and each GPU's HBM moves 2n chunks per call instead of 3n-1 (the result chunk is not
-// read back by the n-1 peers); DONE then also means "my pushes into your recv have landed", and
-// every rank waits for every peer's DONE before its kernel ends.  Only rank r ever writes chunk r
-// of any recv (in place: after its own loads of that slice).  The pushes are sc0 sc1 stores: each
-// is acknowledged once it reached the owner's memory, which drops any copy of the line the owner's
-// L2 kept (file header), and this rank never reads the pushed ranges inside the call.  On the
-// one-GPU proxy: 1.1-1.45x the load form at 2 / 4 / 8 ranks, 1 MiB - 1 GiB
-// (profiles/r3_read_push_ab.txt).  PUSH = false is the load form (READY per iteration, then every
-// peer's result slice loaded over the links), kept as the comparison form.
+// The read schedule's second half: each rank pushes its result slices into every peer's recv
+// (sc0 sc1 stores, straight from the fold's registers) -- no per-iteration READY, no copy phase,
+// and each GPU's HBM moves 2n chunks per call (a load form, every peer reading the result back
+// from the owner's recv, moved 3n-1 and was 1.1-1.45x slower: profiles/r3_read_push_ab.txt); DONE
+// also means "my pushes into your recv have landed", and every rank waits for every peer's DONE
+// before its kernel ends.  Only rank r ever writes chunk r of any recv (in place: after its own
+// loads of that slice).  The pushes are sc0 sc1 stores: each is acknowledged once it reached the
+// owner's memory, which drops any copy of the line the owner's L2 kept (file header), and this
+// rank never reads the pushed ranges inside the call.
 
-template <typename T, int OPC, int G, int V, bool PUSH>
+template <typename T, int OPC, int G, int V>
 __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff, uint32_t nvec, int lane) {
   constexpr uint32_t step = 64 * V;
   const int n = p.n, r = p.rank, w = wave_id().w;
@@ -692,14 +663,12 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
   rsrc_t in[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) in[g] = make_rsrc(p.peer_send[direct_peer(n, r, 1 + (g + 1 < n ? g : 0))] + coff, vb);
-  // PUSH: the result also goes to the same offset of every peer's recv (pipeline w starts at
-  // peer w mod n-1, so a rank's pipelines spread their pushes over all links)
-  rsrc_t pout[PUSH ? G : 1];
-  if (PUSH) {
+  // the result also goes to the same offset of every peer's recv (pipeline w starts at peer
+  // w mod n-1, so a rank's pipelines spread their pushes over all links)
+  rsrc_t pout[G];
 #pragma unroll
-    for (int g = 0; g < G; ++g)
-      pout[g] = make_rsrc(p.peer_recv[direct_peer(n, r, 1 + (g + 1 < n ? (g + w) % (n - 1) : 0))] + coff, vb);
-  }
+  for (int g = 0; g < G; ++g)
+    pout[g] = make_rsrc(p.peer_recv[direct_peer(n, r, 1 + (g + 1 < n ? (g + w) % (n - 1) : 0))] + coff, vb);
   v4u xa[G][V], aa[V], xb[G][V], ab[V];
   auto load = [&](v4u(&x)[G][V], v4u(&a)[V], uint32_t b) {
 #pragma unroll
@@ -720,14 +689,12 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
       }
 #pragma unroll
     for (int u = 0; u < V; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, a[u]);
-    if (PUSH) {
 #pragma unroll
-      for (int g = 0; g < G; ++g)
-        if (g + 1 < n) {
+    for (int g = 0; g < G; ++g)
+      if (g + 1 < n) {
 #pragma unroll
-          for (int u = 0; u < V; ++u) st_slot16(pout[g], (b + (uint32_t)(u * 64 + lane)) * 16, a[u]);
-        }
-    }
+        for (int u = 0; u < V; ++u) st_slot16(pout[g], (b + (uint32_t)(u * 64 + lane)) * 16, a[u]);
+      }
   };
   // The next batch's loads are issued unconditionally: past the slice they fall outside the
   // buffer resources' range, return 0 and touch no memory.  A conditional prefetch made hipcc
@@ -747,8 +714,8 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
   }
 }
 
-// Returns the leading bytes of the slice whose result it also pushed to the peers (PUSH).
-template <typename T, int OPC, bool VEC, bool PUSH>
+// Returns the leading bytes of the slice whose result it also pushed to the peers.
+template <typename T, int OPC, bool VEC>
 __device__ __forceinline__ uint32_t read_fold(const CollParams& p, uint64_t coff, uint32_t nbytes, int lane) {
   if (!VEC) {
     read_fold_scalar<T, OPC>(p, coff, nbytes, lane, 0);
@@ -761,12 +728,12 @@ __device__ __forceinline__ uint32_t read_fold(const CollParams& p, uint64_t coff
     // variants within 256 registers without spilling)
     constexpr int h = sizeof(T) == 2 ? 1 : 0;
     if (!nvec) {
-    } else if (n == 2) read_fold_all<T, OPC, 1, 12 - 4 * h, PUSH>(p, coff, nvec, lane);
-    else if (n == 3) read_fold_all<T, OPC, 2, 8 - 2 * h, PUSH>(p, coff, nvec, lane);
-    else if (n <= 5) read_fold_all<T, OPC, 4, 4 - h, PUSH>(p, coff, nvec, lane);
-    else read_fold_all<T, OPC, 7, 3 - h, PUSH>(p, coff, nvec, lane);
+    } else if (n == 2) read_fold_all<T, OPC, 1, 12 - 4 * h>(p, coff, nvec, lane);
+    else if (n == 3) read_fold_all<T, OPC, 2, 8 - 2 * h>(p, coff, nvec, lane);
+    else if (n <= 5) read_fold_all<T, OPC, 4, 4 - h>(p, coff, nvec, lane);
+    else read_fold_all<T, OPC, 7, 3 - h>(p, coff, nvec, lane);
     if (nbytes & 15u) read_fold_scalar<T, OPC>(p, coff, nbytes, lane, nvec * 16);
-    return PUSH ? nvec * 16 : 0;
+    return nvec * 16;
   }
   constexpr int U = kReadFoldU;
   const rsrc_t out = make_rsrc(p.recv + coff, nbytes);
@@ -801,7 +768,7 @@ __device__ __forceinline__ uint32_t read_fold(const CollParams& p, uint64_t coff
   return 0;
 }
 
-// PUSH, the forms that do not push as they fold: bytes [off0, nbytes) of my result
+// The folds that do not push as they fold (scalar, past 8 ranks): bytes [off0, nbytes) of my result
 // slice, read back from my recv (stored and drained) into every peer's recv
 template <typename T, bool VEC>
 __device__ __forceinline__ void read_push_rest(const CollParams& p, uint64_t coff, uint32_t nbytes, uint32_t off0,
@@ -820,14 +787,13 @@ __device__ __forceinline__ void read_push_rest(const CollParams& p, uint64_t cof
 }
 
 // Messages per (pair, pipeline) and call: START (my send is readable and my recv writable: the
-// call began on my stream), then -- load form only -- READY(t) for t < iters (my result slice of
-// iteration t is in my recv), DONE (I no longer read your buffers, my pushes into your recv have
-// landed: your stream may go on).  Push form per pipeline: START, F0 F1 ... F(I-1), DONE.  Load
-// form: START, F0, F1, G0, F2, G1, ..., G(I-1), DONE -- the next fold's loads leave before this
-// iteration's results are awaited.  The READY word counts iters + 2 messages per call either way
-// (the push form jumps from START to DONE); DONE also returns credits for every message (the
-// scratch schedules' slot counters continue across calls, whatever the schedule).
-template <typename T, int OPC, bool VEC, bool PUSH>
+// call began on my stream), DONE (I no longer read your buffers, my pushes into your recv have
+// landed: your stream may go on).  Per pipeline: START, F0 F1 ... F(I-1), DONE.  The READY word
+// counts iters + 2 messages per call (it jumps from START to DONE: the count the 4.0-5.x load
+// form's per-iteration READYs kept, which the scratch schedules' slot counters still follow);
+// DONE also returns credits for every message (the counters continue across calls, whatever the
+// schedule).
+template <typename T, int OPC, bool VEC>
 __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(CollParams p) {
   signal_start(p);
   const WaveId id = wave_id();
@@ -842,6 +808,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
   const Ctl ctl{p.status, p.host_abort, p.mbox + mbox_abort(n, C), p.timeout_ticks, p.mbox, p.claim};
   const uint32_t iters = p.iters;
   const u64 mpc = read_msgs_per_call(iters);
+  uint32_t seen = 0;  // a cause this wave saw itself (starts_agree), for its ABORT word
   if (lane < n) {
     tx[lane] = p.tx_seq[(u64)lane * C + w];
     rx[lane] = p.rx_seq[(u64)lane * C + w];
@@ -855,59 +822,19 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
   if (!wave_wait_peers(p.mbox + mbox_ready(C, lane, w), rx[lane < n ? lane : 0] + 1, lane < n && lane != r, ctl, lane,
                        true))
     goto aborted;
-  if (!starts_agree(p, ctl, C, lane, w)) goto aborted;
+  if (!starts_agree(p, ctl, C, lane, w, &seen)) goto aborted;
   acquire_sys(p.sys_fence);
-  for (uint32_t j = 0; j <= iters; ++j) {
-    if (j < iters) {
-      // F(j): fold my chunk's slice j from the peers' send buffers, store, drain, READY
-      const u64 s = (u64)j * A + w;
-      const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
-      const u64 coff = (u64)r * p.chunk_bytes + s * p.slice_bytes;
-      const uint32_t pushed = len ? read_fold<T, OPC, VEC, PUSH>(p, coff, len, lane) : 0;
-      if (PUSH) {
-        // no READY (the peers wait only for DONE, which drains every push), so no drain per
-        // slice -- except before the part read back from my recv to be pushed
-        if (pushed < len) {
-          drain_stores();
-          read_push_rest<T, VEC>(p, coff, len, pushed, lane);
-        }
-        continue;
-      }
+  for (uint32_t j = 0; j < iters; ++j) {
+    // F(j): fold my chunk's slice j from the peers' send buffers, store it and push it into every
+    // peer's recv; no READY (the peers wait only for DONE, which drains every push), so no drain
+    // per slice -- except before the part read back from my recv to be pushed
+    const u64 s = (u64)j * A + w;
+    const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
+    const u64 coff = (u64)r * p.chunk_bytes + s * p.slice_bytes;
+    const uint32_t pushed = len ? read_fold<T, OPC, VEC>(p, coff, len, lane) : 0;
+    if (pushed < len) {
       drain_stores();
-      if (p.sys_fence && lane == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      if (lane < n && lane != r) st_sys(p.peer_mbox[lane] + mbox_ready(C, r, w), tx[lane] + 2 + j);
-    }
-    if (!PUSH && j > 0) {
-      // G(j-1): every peer's result slice j-1, peer by peer (pipeline w starts at peer w mod
-      // n-1, so a rank's pipelines spread over all links), into my recv
-      // (full batches peer by peer; the rest of the slice -- all of a short one -- for every
-      // peer at once, once all their READYs are in)
-      const uint32_t t = j - 1;
-      const u64 s = (u64)t * A + w;
-      const uint32_t len = (uint32_t)slice_len(p.chunk_bytes, p.slice_bytes, s);
-      const uint32_t nvec = len >> 4;
-      const uint32_t full = VEC ? nvec / (64u * kReadCopyU) * (64u * kReadCopyU) : 0;
-      for (int k = 1; k < n; ++k) {
-        const int q = direct_peer(n, r, 1 + (k - 1 + w) % (n - 1));
-        if (!wave_wait_ge(p.mbox + mbox_ready(C, q, w), rx[q] + 2 + t, ctl, lane)) goto aborted;
-        acquire_sys(p.sys_fence);
-        const u64 coff = (u64)q * p.chunk_bytes + s * p.slice_bytes;
-        if (VEC && full) {
-          const rsrc_t in = make_rsrc(p.peer_recv[q] + coff, full * 16);
-          move<T, OPC, true, kCopy, kReadCopyU>(nullptr, p.recv + coff, in, in, full * 16, lane);
-        } else if (!VEC && len) {
-          const rsrc_t in = make_rsrc(p.peer_recv[q] + coff, len);
-          move<T, OPC, false, kCopy>(nullptr, p.recv + coff, in, in, len, lane);
-        }
-      }
-      if (VEC && full < nvec) read_copy_wide(p, s * p.slice_bytes, full, nvec, lane);
-      if (VEC && (len & 15u))
-        for (int k = 1; k < n; ++k) {
-          const int q = direct_peer(n, r, k);
-          const u64 coff = (u64)q * p.chunk_bytes + s * p.slice_bytes;
-          const rsrc_t in = make_rsrc(p.peer_recv[q] + coff, len);
-          move_scalar<T, OPC, kCopy>(nullptr, p.recv + coff, in, in, len, lane, nvec * 16);
-        }
+      read_push_rest<T, VEC>(p, coff, len, pushed, lane);
     }
   }
   // DONE: every load of a peer's buffer has returned (and every push into the peers' recv has
@@ -928,7 +855,7 @@ __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) read_kernel(Col
   return;
 aborted:
   if (lane == 0)
-    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), abort_word(p));
+    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), abort_word(p, seen));
 }
 
 // ---------------------------------------------------------------- read schedule, grid form
@@ -959,12 +886,13 @@ __global__ void __launch_bounds__(64) read_start_kernel(CollParams p) {
   const bool peer = lane < n && lane != r;
   const u64 tx = peer ? p.tx_seq[(u64)lane * C] : 0, rx = peer ? p.rx_seq[(u64)lane * C] : 0;
   send_start(p, C, lane, tx + 1, 0);
+  uint32_t seen = 0;
   const bool ok = wave_wait_peers(p.mbox + mbox_ready(C, lane, 0), rx + 1, peer, ctl, lane, true) &&
-                  starts_agree(p, ctl, C, lane, 0);
+                  starts_agree(p, ctl, C, lane, 0, &seen);
   // 0 after a failed START (a graph replay reuses call_seq: the word must not keep a stale "go")
   if (lane == 0) *p.go = ok ? p.call_seq : 0u;
   if (!ok && lane == 0)
-    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), abort_word(p));
+    for (int k = 1; k < n; ++k) st_sys(p.peer_mbox[direct_peer(n, r, k)] + mbox_abort(n, C), abort_word(p, seen));
 }
 
 // one batch of V vectors per lane of my chunk: the peers' slices of it loaded together (G peer
@@ -1275,9 +1203,7 @@ static hipError_t ring_for_t(int op, bool vec, int C, int nt, const CollParams& 
 
 template <typename T>
 static hipError_t read_for_t(int op, bool vec, int C, int nt, const CollParams& p, hipStream_t st) {
-#define READ_LAUNCH(OPC, V)                                                                          \
-  if (p.read_push) hipLaunchKernelGGL((read_kernel<T, OPC, V, true>), dim3(C), dim3(nt), 0, st, p); \
-  else hipLaunchKernelGGL((read_kernel<T, OPC, V, false>), dim3(C), dim3(nt), 0, st, p);
+#define READ_LAUNCH(OPC, V) hipLaunchKernelGGL((read_kernel<T, OPC, V>), dim3(C), dim3(nt), 0, st, p);
 #define READ_CASE(OPC)           \
   case OPC:                      \
     if (vec) {                   \

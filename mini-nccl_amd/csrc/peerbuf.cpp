@@ -26,7 +26,6 @@ namespace {
 constexpr uint32_t kBoardMagic = 0x4d4e4253u;  // 'MNBS'
 constexpr int kBoardDepth = 16;                // records per rank in flight (calls ahead of the slowest peer)
 constexpr int kMaxFreed = 8;                   // freed allocations one record reports (the rest: next calls)
-constexpr size_t kMaxImports = 1024;           // peer allocations mapped per process; beyond: the ring
 constexpr size_t kMaxKnown = 4096;
 constexpr size_t kReapBatch = 4;               // other live exports checked for a free per call
 
@@ -53,6 +52,7 @@ struct alignas(64) CallRec {
   std::atomic<uint64_t> seq;  // the call this record describes; stored last (release)
   uint64_t count;
   int32_t dtype, op, eligible, aligned;
+  int32_t form;  // the kernel form this rank launches for the call (negotiate's `form`)
   BufDesc send, recv;
   int32_t nfreed;
   uint64_t freed[kMaxFreed][2];  // (base, id) of this rank's exported allocations freed since its last record
@@ -316,9 +316,9 @@ char* PeerBuffers::map_peer(int q, uint64_t base, uint64_t id, int fd, const ipc
     if (fd >= 0) close(fd);
     return p;
   }
-  if (ipc::imports() + ipc::retired_imports() >= kMaxImports) {
+  if (ipc::imports() + ipc::retired_imports() >= ipc::kMaxImports) {
     if (fd >= 0) close(fd);
-    *why = "the process maps " + std::to_string(kMaxImports) + " peer allocations already";
+    *why = "the process maps " + std::to_string(ipc::kMaxImports) + " peer allocations already";
     ipc::note_cap_refusal(*why);
     return nullptr;
   }
@@ -363,6 +363,7 @@ void PeerBuffers::publish_fast(uint64_t count, int dtype, int op, uint64_t sig, 
   me.count = count;
   me.dtype = dtype;
   me.op = op;
+  me.form = 0;
   me.eligible = 1;
   me.aligned = 1;
   memset(&me.send, 0, sizeof me.send);
@@ -377,7 +378,7 @@ void PeerBuffers::publish_fast(uint64_t count, int dtype, int op, uint64_t sig, 
 PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv, bool eligible, uint64_t count,
                                              int dtype, int op, double timeout_s,
                                              const std::function<void()>& sync_previous, const char** psend,
-                                             const char** precv, bool* vec_all) {
+                                             const char** precv, bool* vec_all, int form) {
   const uint64_t k = ++seq_;
   const double t0 = now_s();
   // spins until ready() -- bounded by the peer q giving up and by the rendezvous limit
@@ -393,7 +394,8 @@ PeerBuffers::Decision PeerBuffers::negotiate(const void* send, const void* recv,
     }
   };
   try {
-    return negotiate_body(k, send, recv, eligible, count, dtype, op, sync_previous, psend, precv, vec_all, wait_for);
+    return negotiate_body(k, send, recv, eligible, count, dtype, op, form, sync_previous, psend, precv, vec_all,
+                          wait_for);
   } catch (...) {
     // this rank gives up (a peer that never came or gave up itself): say so on the board, so
     // every peer waiting in a rendezvous with it fails at once instead of at its own limit (the
@@ -520,7 +522,7 @@ PeerBuffers::Pending PeerBuffers::take_fds(int q, uint64_t k, const WaitFn& wait
 
 template <typename WaitFor>
 PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible,
-                                                  uint64_t count, int dtype, int op,
+                                                  uint64_t count, int dtype, int op, int form,
                                                   const std::function<void()>& sync_previous, const char** psend,
                                                   const char** precv, bool* vec_all, const WaitFor& wait_for) {
   auto wait = [&](const std::atomic<uint64_t>& v, uint64_t want, int q, const char* what) {
@@ -544,6 +546,7 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
   me.count = count;
   me.dtype = dtype;
   me.op = op;
+  me.form = form;
   me.fast = 0;
   me.sig = 0;
   me.eligible = ok ? 1 : 0;
@@ -561,7 +564,7 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
 
   struct Seen {
     uint64_t count;
-    int32_t dtype, op, eligible, aligned, fast;
+    int32_t dtype, op, eligible, aligned, fast, form;
     BufDesc send, recv;
     int32_t nfreed;
     uint64_t freed[kMaxFreed][2];
@@ -577,6 +580,7 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
     s.eligible = c.eligible;
     s.aligned = c.aligned;
     s.fast = c.fast;
+    s.form = c.form;
     s.send = c.send;
     s.recv = c.recv;
     s.nfreed = c.nfreed < 0 ? 0 : c.nfreed > kMaxFreed ? kMaxFreed : c.nfreed;
@@ -619,7 +623,7 @@ PeerBuffers::Decision PeerBuffers::negotiate_body(uint64_t k, const void* send, 
   for (const Seen& c : recs) {
     all = all && c.eligible;
     aligned = aligned && c.aligned;
-    mismatch = mismatch || c.count != count || c.dtype != dtype || c.op != op;
+    mismatch = mismatch || c.count != count || c.dtype != dtype || c.op != op || c.form != form;
   }
   const Decision d = mismatch ? kMismatch : all ? kRead : kFallback;
   *vec_all = aligned;

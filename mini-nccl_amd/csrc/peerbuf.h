@@ -61,11 +61,14 @@ class PeerBuffers {
   // also requires them to be memory of this rank's GPU, and shareable).  On kRead, psend /
   // precv[q] hold rank q's buffers mapped here (this rank's own at [rank]) and *vec_all whether
   // every rank's buffers are dword-aligned.  `sync_previous` waits for this communicator's last
-  // kernel (before a freed peer allocation's mapping is closed).  Throws std::runtime_error when
-  // a peer does not arrive within timeout_s.
+  // kernel (before a freed peer allocation's mapping is closed).  `form`: the kernel form this
+  // rank would launch for the call (Comm: its schedule choice, mncclCommSetAlgo) -- ranks that
+  // differ in it get kMismatch, as for count / dtype / op (a grid-form rank's DONE could otherwise
+  // be met by a persistent peer's pipeline 0 while the other pipelines never start).  Throws
+  // std::runtime_error when a peer does not arrive within timeout_s.
   Decision negotiate(const void* send, const void* recv, bool eligible, uint64_t count, int dtype, int op,
                      double timeout_s, const std::function<void()>& sync_previous, const char** psend,
-                     const char** precv, bool* vec_all);
+                     const char** precv, bool* vec_all, int form = 0);
 
   // A registered-window call (Comm::allreduce's fast path): this rank's record for the next call,
   // marked fast with the call's signature, published WITHOUT reading the peers' -- their kernels
@@ -110,8 +113,8 @@ class PeerBuffers {
   using WaitFn = std::function<void(const std::function<bool()>&, int, const char*)>;
   template <typename WaitFor>
   Decision negotiate_body(uint64_t k, const void* send, const void* recv, bool eligible, uint64_t count, int dtype,
-                          int op, const std::function<void()>& sync_previous, const char** psend, const char** precv,
-                          bool* vec_all, const WaitFor& wait_for);
+                          int op, int form, const std::function<void()>& sync_previous, const char** psend,
+                          const char** precv, bool* vec_all, const WaitFor& wait_for);
   bool describe(const void* p, uint64_t* base, uint64_t* id, ipc::Shared* d);
   char* map_peer(int q, uint64_t base, uint64_t id, int fd, const ipc::Shared& d, std::string* why);
   void sock_addr(int q, void* addr, unsigned* len) const;

@@ -88,10 +88,9 @@ MNCCL_HD RingOp ring_op(int n, int r, int k) {
 MNCCL_HD int direct_peer(int n, int r, int k) { return mod_n(r + k, n); }  // k = 1..n-1
 
 // Read schedule (MINI_NCCL_ALGO=read): no scratch; rank r loads the peers' raw slices of chunk
-// r straight from their send buffers and stores the result into every rank's recv (push form)
-// or each peer loads it from r's recv after a READY (load form, MINI_NCCL_READ_PUSH=0).
-// Messages per (pair, pipeline) and call, all on the READY word: START, one per iteration (load
-// form only; the push form skips them), DONE.
+// r straight from their send buffers and stores the result into every rank's recv.  Messages per
+// (pair, pipeline) and call, all on the READY word: START and DONE; the count advances by
+// iters + 2 (the 4.0-5.x load form also sent one READY per iteration; every rank counts alike).
 MNCCL_HD uint64_t read_msgs_per_call(uint32_t iters) { return (uint64_t)iters + 2; }
 
 // Pipelines a call runs (ring and read alike): one per slice, up to all C of them, rounded up to
@@ -291,9 +290,9 @@ MNCCL_HD int topology_blocks_read(int n, const int* link, const int* hops) {
 // persistent kernel's bimodal placement), 4 ranks 1.04x, 8 ranks 0.99-1.02x
 // (profiles/r5_read_vs_grid_forms.txt, r5_bench_n{2,8}_auto_grid.json).  Uniform across ranks:
 // every input is.
-MNCCL_HD bool read_grid_form(bool forced, bool auto_mode, bool push, bool vec, uint64_t chunk_bytes, int n,
+MNCCL_HD bool read_grid_form(bool forced, bool auto_mode, bool vec, uint64_t chunk_bytes, int n,
                              uint64_t min_bytes = kReadGridMin) {
-  return (forced || auto_mode) && push && vec && read_grid_fits(chunk_bytes, n, min_bytes);
+  return (forced || auto_mode) && vec && read_grid_fits(chunk_bytes, n, min_bytes);
 }
 
 // Kernel status bits (host-mapped status word)

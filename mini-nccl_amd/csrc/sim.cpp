@@ -30,7 +30,6 @@ float apply(int op, float a, float b) {
 struct World {
   int n, C, K, op, algo;
   int A = 0;  // pipelines the current call runs (schedule.h call_pipelines)
-  bool push = true;  // read schedule: push form (kernels.hip PUSH) or load form
   uint64_t slice, slot_bytes, chunk_bytes, nslices;  // payload per message, slot stride
   uint32_t iters;
   std::vector<const float*> send;
@@ -68,7 +67,7 @@ void do_move(int kind, int op, const float* local, const float* in, float* recv,
 struct Prog {
   int r, w;
   uint32_t it = 0;
-  int k = 0;      // ring: op index within the iteration; read (load form): 0 = fold, 1..n-1 = copy from peer k
+  int k = 0;      // ring: op index within the iteration
   uint32_t j = 0; // read: stage
   bool done = false;
 };
@@ -106,19 +105,16 @@ bool ring_step(World& W, Prog& P) {
 
 // One step of the read schedule (kernels.hip read_kernel): stage 0 publishes START, 1 waits for
 // every peer's START, 2 runs the iterations, 3 publishes DONE (+ credits), 4 waits for every
-// peer's DONE.  Push form (W.push): one step per iteration -- the fold of slice it of chunk r
-// from the peers' send buffers, stored into this rank's recv AND into every peer's recv at the
-// same offset, no READY.  Load form: the fold of iteration t stores into this rank's recv and
-// raises READY(t); then, one step per peer (pipeline w starts at peer w mod n-1), each peer's
-// result slice t-1 is copied out of that peer's recv once its READY(t-1) is seen.  Every peer
-// access touches the peer's own buffers (W.send / W.recv of that rank), so an in-place call whose
-// order were wrong would read overwritten data and fail the oracle comparison.
+// peer's DONE.  One step per iteration -- the fold of slice it of chunk r from the peers' send
+// buffers, stored into this rank's recv AND pushed into every peer's recv at the same offset, no
+// READY.  Every peer access touches the peer's own buffers (W.send / W.recv of that rank), so an
+// in-place call whose order were wrong would read overwritten data and fail the oracle comparison.
 bool read_step(World& W, Prog& P) {
   const int n = W.n, r = P.r, w = P.w;
   auto tx = [&](int d) { return W.tx_seq[r][(size_t)d * W.C + w]; };
   auto rx = [&](int q) { return W.rx_seq[r][(size_t)q * W.C + w]; };
   const uint64_t mpc = read_msgs_per_call(W.iters);
-  auto fold = [&](uint32_t it, bool push) {  // slice `it` of chunk r, stored (and pushed)
+  auto fold = [&](uint32_t it) {  // slice `it` of chunk r, stored and pushed
     const uint64_t s = (uint64_t)it * W.A + w;
     const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
     const uint64_t coff = (uint64_t)r * W.chunk_bytes + s * W.slice;
@@ -135,8 +131,7 @@ bool read_step(World& W, Prog& P) {
     // every load of the slice came first (in place, recv chunk r of a peer is its send chunk r)
     if (len) {
       memcpy((char*)W.recv[r] + coff, res.data(), (size_t)len);
-      if (push)
-        for (int k = 1; k < n; ++k) memcpy((char*)W.recv[direct_peer(n, r, k)] + coff, res.data(), (size_t)len);
+      for (int k = 1; k < n; ++k) memcpy((char*)W.recv[direct_peer(n, r, k)] + coff, res.data(), (size_t)len);
     }
   };
   switch (P.j) {
@@ -173,32 +168,8 @@ bool read_step(World& W, Prog& P) {
       P.k = 0;
       return true;
     case 2:
-      if (W.push) {
-        if (P.it < W.iters) fold(P.it++, true);
-        if (P.it >= W.iters) P.j = 3;
-        return true;
-      }
-      if (P.k == 0) {
-        if (P.it < W.iters) {
-          fold(P.it, false);
-          for (int k = 1; k < n; ++k) W.ready(direct_peer(n, r, k), r, w) = tx(direct_peer(n, r, k)) + 2 + P.it;
-        }
-        if (P.it > 0) P.k = 1;
-        else ++P.it;
-      } else {
-        const uint32_t t = P.it - 1;
-        const int q = direct_peer(n, r, 1 + (P.k - 1 + w) % (n - 1));
-        if (W.ready(r, q, w) < rx(q) + 2 + t) return false;
-        const uint64_t s = (uint64_t)t * W.A + w;
-        const uint64_t len = slice_len(W.chunk_bytes, W.slice, s);
-        const uint64_t coff = (uint64_t)q * W.chunk_bytes + s * W.slice;
-        memcpy((char*)W.recv[r] + coff, (const char*)W.recv[q] + coff, len);
-        if (++P.k == n) {
-          P.k = 0;
-          ++P.it;
-        }
-      }
-      if (P.it > W.iters) P.j = 3;
+      if (P.it < W.iters) fold(P.it++);
+      if (P.it >= W.iters) P.j = 3;
       return true;
     case 3:
       for (int k = 1; k < n; ++k) {
@@ -300,14 +271,13 @@ int mnccl_call_pipelines(uint64_t nslices, int channels, int waves) { return cal
 
 // schedule.h topology_blocks_read over an n x n matrix (rank q's row: how q's GPU reaches p's)
 int mnccl_topology_blocks_read(int n, const int* link, const int* hops) { return topology_blocks_read(n, link, hops); }
-int mnccl_read_grid_form(int forced, int auto_mode, int push, int vec, uint64_t chunk_bytes, int n,
-                         uint64_t min_bytes) {
-  return read_grid_form(forced != 0, auto_mode != 0, push != 0, vec != 0, chunk_bytes, n, min_bytes) ? 1 : 0;
+int mnccl_read_grid_form(int forced, int auto_mode, int vec, uint64_t chunk_bytes, int n, uint64_t min_bytes) {
+  return read_grid_form(forced != 0, auto_mode != 0, vec != 0, chunk_bytes, n, min_bytes) ? 1 : 0;
 }
 
 // Runs `calls` consecutive all-reduces (send -> recv, fp32; send == recv for in place) on n
 // simulated ranks with the GPU kernels' protocol; call i uses schedule (algo >> 3i) & 7 (0 ring,
-// 1 one-shot, 2 read in its push form, 3 read in its load form, 4 read's grid form -- START and
+// 1 one-shot, 2 read (persistent kernel), 4 read's grid form (3, the 4.0-5.x load form, is gone) -- START and
 // DONE on pipeline 0, the whole chunk folded and pushed between them, as kernels.hip
 // read_start / read_grid / read_done do; schedules can alternate on one communicator state, as
 // mncclCommSetAlgo allows; at most 21 calls).  A one-shot call's slice: oneshot_slice when
@@ -334,9 +304,8 @@ int mnccl_sim_allreduce(uint64_t algo, const float* const* send, float* const* r
   uint64_t rng = schedule_seed * 6364136223846793005ull + 1442695040888963407ull;
   for (int call = 0; call < calls; ++call) {
     const int code = (int)((algo >> (3 * call)) & 7);
-    if (code > 4) return -2;
+    if (code > 4 || code == 3) return -2;
     const int a = code >= 2 ? 2 : code;  // 0 ring, 1 one-shot, 2 read
-    W.push = code == 2 || code == 4;
     // as Comm::launch: adaptive payload (min_slice 0 = off; the read schedule's own rule), fixed
     // slot stride, one pipeline per slice up to all of them
     if (a == 1 && W.chunk_bytes) {
@@ -419,7 +388,7 @@ int mnccl_sim_signed_read(const float* const* send, float* const* recv, int n, u
                           uint64_t slice_bytes, const uint64_t* sigs, uint64_t schedule_seed, int* mismatch_out) {
   if (n < 2 || n > 16 || channels < 1 || slice_bytes < 4 || slice_bytes % 4) return -2;
   World W;
-  W.n = n; W.C = channels; W.K = 2; W.op = 0; W.algo = 2; W.slot_bytes = slice_bytes; W.push = true;
+  W.n = n; W.C = channels; W.K = 2; W.op = 0; W.algo = 2; W.slot_bytes = slice_bytes;
   W.chunk_bytes = count / (uint64_t)n * 4;
   W.send.assign(send, send + n);
   W.recv.assign(recv, recv + n);

@@ -62,6 +62,9 @@ class CommInfo(ctypes.Structure):
         ("window_calls", ctypes.c_ulonglong), ("windows", ctypes.c_int), ("auto_grid", ctypes.c_int),
         # since mncclVersion 501
         ("retired_imports", ctypes.c_int),
+        # since mncclVersion 600
+        ("retired_bytes", ctypes.c_ulonglong), ("retired_budget", ctypes.c_ulonglong),
+        ("budget_refusals", ctypes.c_ulonglong),
     ]
 
 

@@ -285,6 +285,48 @@ def release_rank(rank, n, port, env, nbytes, out_q, barrier=None):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def churn_rank(rank, n, port, env, calls, nbytes, out_q, barrier=None):
+    """VERDICT r5 #3 / ADVICE r5: `calls` all-reduces, each on a FRESH in-place allocation of `nbytes`
+    that is freed right after its call (no caching allocator: every call brings buffers new to the
+    peers).  Co-located ranks retire their imports of each other's freed buffers (csrc/ipcreg.h),
+    so the retired budget (MINI_NCCL_RETIRED_MB) or the import count cap must take the later calls
+    to the ring.  Integer-valued data (sums exact in any order), every element checked; the
+    device's free memory sampled after every call."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        use_rank_device(rank)
+        comm = M.Comm(n, rank, "127.0.0.1")
+        st = hip_rt.Stream()
+        count = nbytes // 4
+        base = (np.arange(count, dtype=np.int64) % 1021).astype(np.float32)
+        hip_rt.sync()
+        barrier.wait(120)
+        free0, _ = hip_rt.mem_get_info()
+        min_free, rcs, algos, bad = free0, [], [], 0
+        for i in range(calls):
+            buf = hip_rt.DeviceBuffer(nbytes, fresh=True)
+            buf.upload(base + np.float32(7 * rank + i % 13))
+            rc = comm.all_reduce(buf.ptr, buf.ptr, count, M.ncclFloat, M.ncclSum, st.handle)
+            st.sync()
+            rcs.append(rc)
+            algos.append(comm.info()["last_algo"])
+            want = n * base + np.float32(sum(7 * q + i % 13 for q in range(n)))
+            got = buf.download(np.float32, count)
+            bad += int((got != want).sum())
+            buf.free()
+            hip_rt.sync()
+            min_free = min(min_free, hip_rt.mem_get_info()[0])
+        info = comm.info()
+        st.destroy()
+        out_q.put((rank, {"rcs": rcs, "algos": algos, "bad": bad, "free0": free0, "min_free": min_free,
+                          "info": info, "destroy": comm.destroy()}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
 def two_comms_rank(rank, n, ports, env, rounds, out_q):
     """Two communicators in one process sharing the same send / recv buffers, calls alternating
     between them; every other round on fresh allocations (freed after it).  Each communicator

@@ -53,7 +53,7 @@ static int sim_case(int algo, int n, uint64_t count, uint64_t slice, uint64_t mi
 int main() {
   int fails = 0;
   const uint64_t counts[] = {7, 1000, 4099, 70001};
-  for (int algo : {0, 2, 3, 4})  // ring, read (push form), read (load form), read's grid form
+  for (int algo : {0, 2, 4})  // ring, read (persistent kernel), read's grid form
     for (int n = 2; n <= 8; n += 3)
       for (uint64_t c : counts)
         for (int adaptive = 0; adaptive < 2; ++adaptive) {

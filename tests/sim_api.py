@@ -25,7 +25,7 @@ def load():
         L.mnccl_read_slice.restype = u64
         L.mnccl_call_pipelines.argtypes = [u64, i, i]
         L.mnccl_topology_blocks_read.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(i)]
-        L.mnccl_read_grid_form.argtypes = [i, i, i, i, u64, i, u64]
+        L.mnccl_read_grid_form.argtypes = [i, i, i, u64, i, u64]
         L.mnccl_sim_signed_read.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64,
                                             ctypes.POINTER(u64), u64, ctypes.POINTER(i)]
         L.mnccl_oneshot_slice.argtypes = [u64, i, i, u64]
@@ -41,14 +41,14 @@ def load():
 
 
 # schedules: the ring, the one-shot, read in its push form, read in its load form, read's grid form
-RING, ONESHOT, READ, READ_LOAD, READ_GRID = 0, 1, 2, 3, 4
+RING, ONESHOT, READ, READ_GRID = 0, 1, 2, 4  # (3: the load form, removed in 6.0)
 
 
 def allreduce(inputs, algo=0, op=0, slice_bytes=1024, channels=4, slots=2, calls=1, seed=0, algos=None, min_slice=0,
               inplace=False):
     """fp32 all-reduce of `inputs` (one array per rank) through the simulated kernels,
-    `calls` times on one communicator state (schedule `algo` -- RING, ONESHOT, READ (push form),
-    READ_LOAD (MINI_NCCL_READ_PUSH=0) or READ_GRID (the push form's grid launches) -- for every
+    `calls` times on one communicator state (schedule `algo` -- RING, ONESHOT, READ (the
+    persistent kernel) or READ_GRID (its grid launches) -- for every
     call, or the per-call list `algos`; at most 21 calls).  inplace: send == recv (then every call after the first reduces the previous
     result).  Returns (outputs, steps); raises RuntimeError on deadlock."""
     if algos is None:
@@ -146,8 +146,8 @@ def signed_read(inputs, sigs, slice_bytes=1024, channels=4, seed=1):
     return recvs, list(mm)
 
 
-def read_grid_form(forced, auto_mode, push, vec, chunk_bytes, n, min_bytes=4 << 20):
+def read_grid_form(forced, auto_mode, vec, chunk_bytes, n, min_bytes=4 << 20):
     """csrc/schedule.h read_grid_form: a read-schedule call launches in the grid form (chunks of
     at least min_bytes: MINI_NCCL_GRID_MIN, default kReadGridMin = 4 MiB)."""
-    return bool(load().mnccl_read_grid_form(int(forced), int(auto_mode), int(push), int(vec), chunk_bytes, n,
+    return bool(load().mnccl_read_grid_form(int(forced), int(auto_mode), int(vec), chunk_bytes, n,
                                             min_bytes))

@@ -93,7 +93,7 @@ def test_argument_checks_before_device_work(nccl_lib):
     assert L.mncclLocalReduce(fake, fake, fake, 4, M.ncclFloat, M.ncclAvg, None) == M.ncclInternalError
     assert L.mncclLocalReduce(None, fake, fake, 4, M.ncclFloat, M.ncclSum, None) == M.ncclInvalidArgument
     assert L.mncclCommSetAlgo(None, 0) == M.ncclInvalidArgument
-    assert L.mncclVersion() == 501
+    assert L.mncclVersion() == 600
 
 
 def test_info_struct_layout(nccl_lib):
@@ -151,7 +151,7 @@ def test_config_from_env(sim_lib, monkeypatch):
     # reference defaults (Config.h:29-47): 128 KiB, 64, 16; workgroups derived per communicator
     # (channels=0, schedule.h pipeline_geometry); no auto-tune at init; 512 MiB scratch cap
     assert "SLICE_SIZE=131072 B" in s and "WINDOW=64" in s and "BATCH=16" in s and "channels=0" in s
-    assert "algo=auto" in s and "threads=64" in s and "sys_fence=0" in s and "read_push=1" in s
+    assert "algo=auto" in s and "threads=64" in s and "sys_fence=0" in s and "read_push" not in s
     assert "scratch_cap=512 MiB" in s
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", "0")       # Config.h:50: 0 -> 1024
     monkeypatch.setenv("MINI_NCCL_WINDOW_SIZE", "-3")     # Config.h:51: <= 0 -> 1
@@ -163,9 +163,9 @@ def test_config_from_env(sim_lib, monkeypatch):
     assert rc == 0 and f"SLICE_SIZE={256 << 20} B" in s
     monkeypatch.setenv("MINI_NCCL_ALGO", "ring")
     monkeypatch.setenv("MINI_NCCL_SLICE_SIZE", "100")     # rounded down to whole 16-byte vectors
-    monkeypatch.setenv("MINI_NCCL_READ_PUSH", "0")        # the read schedule's load form
+    monkeypatch.setenv("MINI_NCCL_READ_PUSH", "0")        # the load form, removed in 6.0: warned, ignored
     rc, s = S.config_describe()
-    assert "algo=ring" in s and "SLICE_SIZE=96 B" in s and "read_push=0" in s
+    assert rc == 0 and "algo=ring" in s and "SLICE_SIZE=96 B" in s
     monkeypatch.setenv("MINI_NCCL_ALGO", "direct")        # removed in 4.0: an init error, not a silent ring
     rc, s = S.config_describe()
     assert rc == -1 and "no longer" in s

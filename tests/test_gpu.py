@@ -5,9 +5,8 @@
 * ncclAllReduce with 2-10 rank processes, rank r on GPU r % ndev (one rank per GPU on a
   multi-GPU box: a cross-device run over xGMI) or all on GPU 0 on a 1-GPU box / under
   MNCCL_TEST_COLOCATE=1 (as the reference's perf_test does, tests/perf_test.cpp:46), every
-  rank's device and co-located rank count checked against that placement; the ring and the
-  read schedule (push form, and its load
-  form MINI_NCCL_READ_PUSH=0 where the protocol differs), in/out of place, odd counts
+  rank's device and co-located rank count checked against that placement; the ring, the
+  read schedule (persistent and grid forms) and the one-shot, in/out of place, odd counts
   (tail), repeated calls, slices smaller than a chunk, bit-exact vs the oracle (NaN
   payloads of +/* excepted: NaN-ness must match);
 * error paths: watchdog timeout -> ncclInternalError and a sticky error afterwards.
@@ -25,10 +24,8 @@ pytestmark = pytest.mark.gpu
 
 DTYPES = ["f32", "f64", "i32", "f16", "bf16"]
 OPS = ["sum", "prod", "max", "min"]
-LOAD_FORM = {"MINI_NCCL_READ_PUSH": "0"}
-# (schedule, extra environment): the ring, read (push form, the default), read's load form
+# (schedule, extra environment): the ring, read (the default's persistent kernel)
 SCHEDULES = [pytest.param((0, {}), id="ring"), pytest.param((2, {}), id="read")]
-SCHEDULES_ALL = SCHEDULES + [pytest.param((2, LOAD_FORM), id="read_load")]
 
 
 @pytest.fixture(scope="module")
@@ -123,7 +120,7 @@ def _case(dtype="f32", op="sum", count=1 << 18, inplace=False, algo=0, calls=1, 
                 offset=offset, **kw)
 
 
-@pytest.mark.parametrize("sched", SCHEDULES_ALL)
+@pytest.mark.parametrize("sched", SCHEDULES)
 @pytest.mark.parametrize("n", [2, 3, 4])
 def test_allreduce_fp32_sum(dev, n, sched):
     algo, env = sched
@@ -156,7 +153,7 @@ def test_host_buffers(dev, algo):
     _run_allreduce(3, cases)
 
 
-@pytest.mark.parametrize("sched", SCHEDULES_ALL + [pytest.param((3, {}), id="oneshot")])
+@pytest.mark.parametrize("sched", SCHEDULES + [pytest.param((3, {}), id="oneshot")])
 @pytest.mark.parametrize("blocking", ["1", "0"], ids=["blocking", "async"])
 def test_skewed_ranks_varying_data(dev, sched, blocking):
     algo, env = sched
@@ -186,8 +183,10 @@ def test_auto_schedule_no_init_allreduce(dev):
         assert i["channels"] == 256 and i["pipelines"] == 256 and i["slot_bytes"] == 128 << 10
         assert i["scratch_bytes"] == 2 * 256 * 2 * (128 << 10)  # (n-1) peer regions
     port = GW.free_port()
-    out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {"MINI_NCCL_ALGO": "ring", **LOAD_FORM}), 120)
-    assert out[0]["info"]["algo"] == 0 and out[0]["info"]["read_push"] == 0
+    out = GW.run_ranks(GW.info_rank, 3, lambda r: (r, 3, port, {"MINI_NCCL_ALGO": "ring", "MINI_NCCL_READ_PUSH": "0"}),
+                       120)
+    # (MINI_NCCL_READ_PUSH: the load form was removed in 6.0 -- the knob is warned about and ignored)
+    assert out[0]["info"]["algo"] == 0 and out[0]["info"]["read_push"] == 1
     # MINI_NCCL_ALGO=direct (removed in 4.0) fails init instead of silently running another schedule
     import mini_nccl as M
     port = GW.free_port()
@@ -204,7 +203,7 @@ def test_sys_fence_on(dev, algo):
     _run_allreduce(3, cases, env={"MINI_NCCL_SYS_FENCE": "1"})
 
 
-@pytest.mark.parametrize("sched", SCHEDULES_ALL)
+@pytest.mark.parametrize("sched", SCHEDULES)
 def test_allreduce_8_ranks(dev, sched):
     algo, env = sched
     # the 8-GPU node's rank count, all on GPU 0 at the library's default geometry (256
@@ -261,7 +260,7 @@ def test_allreduce_slice_points(dev, slice_kib, n, algo):
     _run_allreduce(n, cases, env={"MINI_NCCL_SLICE_SIZE": str(sl), "MINI_NCCL_CHANNELS": "16"}, timeout=600)
 
 
-@pytest.mark.parametrize("sched", SCHEDULES_ALL)
+@pytest.mark.parametrize("sched", SCHEDULES)
 def test_allreduce_dtypes_ops(dev, sched):
     algo, env = sched
     cases = [_case(dtype=d, op=o, count=50000 + 7 * i, algo=algo, seed=100 + i, special=o in ("max", "min"))
@@ -301,9 +300,8 @@ def test_oneshot_10_ranks(dev):
     _run_allreduce(10, cases, env, timeout=600)
 
 
-@pytest.mark.parametrize("n,algo,env", [(2, 2, {}), (3, 2, {}), (8, 2, {"GPU_MAX_HW_QUEUES": "2"}),
-                                        (3, 2, LOAD_FORM), (3, 0, {})],
-                         ids=["read_n2", "read_n3", "read_n8", "read_load_n3", "ring_n3"])
+@pytest.mark.parametrize("n,algo,env", [(2, 2, {}), (3, 2, {}), (8, 2, {"GPU_MAX_HW_QUEUES": "2"}), (3, 0, {})],
+                         ids=["read_n2", "read_n3", "read_n8", "ring_n3"])
 def test_read_push_visible_to_cached_consumers(dev, n, algo, env):
     # recv's lines pre-warmed into its owner's L2 by an ordinary kernel, then a call
     # whose peers push into that recv (other GPUs over xGMI when the placement spreads the ranks,
@@ -531,6 +529,61 @@ def test_same_gpu_freed_imports_leave_later_exports_intact(dev):
             assert res[-1]["retired_imports"] >= res[-1]["closed_freed"] > 0, res[-1]
 
 
+def _churn(n, env, calls, nbytes, timeout):
+    port = GW.free_port()
+    e = {"MINI_NCCL_TIMEOUT_MS": "30000", **env}
+    out = GW.run_ranks(GW.churn_rank, n, lambda r: (r, n, port, e, calls, nbytes), timeout, barrier=True)
+    assert sorted(out) == list(range(n)), out
+    for r in range(n):
+        assert "error" not in out[r], out[r]["error"]
+        o = out[r]
+        _check_placement(r, n, o["info"])
+        assert o["destroy"] == 0 and o["rcs"] == [0] * calls and o["bad"] == 0, (r, o["bad"], o["rcs"][:8])
+        assert o["info"]["ipc_open_failures"] == 0, o["info"]
+    return out
+
+
+def test_retired_imports_bounded_by_byte_budget(dev):
+    # 2 ranks, 200 calls, each on a fresh 64 MiB allocation freed after it.  Co-located,
+    # every peer import of a freed buffer stays mapped (the driver's shared handle, csrc/ipcreg.h):
+    # MINI_NCCL_RETIRED_MB = 1024 bounds what that pins -- the calls past it run the ring on every
+    # rank alike, counted in budget_refusals, each still exact -- and the device's free memory never
+    # drops by more than both processes' budgets plus the live buffers
+    n, calls, nbytes, budget = 2, 200, 64 << 20, 1024 << 20
+    out = _churn(n, {"MINI_NCCL_RETIRED_MB": str(budget >> 20)}, calls, nbytes, 600)
+    for r in range(n):
+        o, i = out[r], out[r]["info"]
+        if i["ranks_on_device"] == 1:  # a GPU of its own: nothing is retired, every call reads
+            assert i["retired_bytes"] == 0 and set(o["algos"]) == {2}, (r, i["retired_bytes"], o["algos"][:8])
+            continue
+        assert i["retired_budget"] == budget, i["retired_budget"]
+        assert budget <= i["retired_bytes"] <= budget + nbytes, i["retired_bytes"]
+        assert i["budget_refusals"] > 0, i
+        k = o["algos"].index(0)  # the first ring call: past the budget, every call the ring
+        assert set(o["algos"][:k]) == {2} and set(o["algos"][k:]) == {0}, o["algos"]
+        assert k <= budget // nbytes + 2, k
+        drop = o["free0"] - o["min_free"]
+        assert drop <= n * (budget + 2 * nbytes) + (512 << 20), (drop >> 20, "MiB")
+
+
+def test_freed_peer_buffers_beyond_the_import_cap(dev):
+    # more freed peer allocations than the import cap (1024, live + retired) across
+    # co-located ranks: past the cap every call runs the ring (cap_refusals), still exact, and the
+    # memory the retired imports hold is recorded (small buffers: the byte budget is not the bound)
+    n, calls, nbytes = 2, 1100, 64 << 10
+    out = _churn(n, {}, calls, nbytes, 600)
+    for r in range(n):
+        o, i = out[r], out[r]["info"]
+        if i["ranks_on_device"] == 1:
+            assert i["retired_imports"] == 0 and set(o["algos"]) == {2}
+            continue
+        assert i["retired_imports"] >= 1000 and i["retired_bytes"] >= i["retired_imports"] * nbytes, i
+        assert i["cap_refusals"] > 0 and i["budget_refusals"] == 0, i
+        # (the read schedule's fallback for a call this small under auto: the one-shot, else the ring)
+        assert o["algos"][:900] == [2] * 900 and set(o["algos"][-50:]) <= {0, 3}, o["algos"][895:910]
+        print(f"rank {r}: {i['retired_imports']} retired imports hold {i['retired_bytes'] >> 20} MiB")
+
+
 def test_read_schedule_send_recv_in_one_allocation(dev):
     # out of place with send and recv two regions of ONE allocation on every rank: the owner's
     # descriptor datagram carries that allocation once, both mappings come from one import;
@@ -751,7 +804,7 @@ def test_single_rank_is_copy_only(dev):
 
 
 @pytest.mark.parametrize("knob,values", [("MINI_NCCL_SLICE_SIZE", ("131072", "65536")),
-                                         ("MINI_NCCL_READ_PUSH", ("1", "0")), ("MINI_NCCL_ALGO", ("ring", "oneshot")),
+                                         ("MINI_NCCL_ALGO", ("ring", "oneshot")),
                                          ("MINI_NCCL_WINDOW_SIZE", ("64", "16")),
                                          ("MINI_NCCL_GRID_MIN", (str(4 << 20), str(1 << 20)))])
 def test_mismatched_config_is_system_error(dev, knob, values):

@@ -20,7 +20,7 @@ def same_bits(a, b):
     return np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
 
 
-@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_LOAD], ids=["ring", "read", "read_load"])
+@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_GRID], ids=["ring", "read", "read_grid"])
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
 @pytest.mark.parametrize("count,slice_bytes,channels,slots", [
     (4096, 256, 4, 2),      # several slices per channel
@@ -37,7 +37,7 @@ def test_sim_matches_oracle(oracle_lib, sim_lib, algo, n, count, slice_bytes, ch
         assert same_bits(got[r], ref[r]), f"rank {r}"
 
 
-@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_LOAD], ids=["ring", "read", "read_load"])
+@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_GRID], ids=["ring", "read", "read_grid"])
 @pytest.mark.parametrize("op", OPS)
 def test_sim_all_ops(oracle_lib, sim_lib, algo, op):
     xs = O.random_inputs(4, 2050, "f32", seed=11)
@@ -46,7 +46,7 @@ def test_sim_all_ops(oracle_lib, sim_lib, algo, op):
     assert all(same_bits(g, e) for g, e in zip(got, ref))
 
 
-@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_LOAD], ids=["ring", "read", "read_load"])
+@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_GRID], ids=["ring", "read", "read_grid"])
 @pytest.mark.parametrize("seed", range(1, 13))
 def test_sim_random_interleavings_no_deadlock(oracle_lib, sim_lib, algo, seed):
     n = 2 + seed % 7
@@ -57,7 +57,7 @@ def test_sim_random_interleavings_no_deadlock(oracle_lib, sim_lib, algo, seed):
     assert all(same_bits(g, e) for g, e in zip(got, ref))
 
 
-@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_LOAD], ids=["ring", "read", "read_load"])
+@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_GRID], ids=["ring", "read", "read_grid"])
 def test_sim_sequence_continues_across_calls(oracle_lib, sim_lib, algo):
     # 5 calls on one communicator state: flags are monotone and never reset
     xs = O.random_inputs(4, 5000, "f32", seed=5)
@@ -88,7 +88,7 @@ def test_single_slot_fifo_deadlocks(sim_lib):
         S.allreduce(xs, algo=S.RING, slice_bytes=256, channels=2, slots=1)
 
 
-@pytest.mark.parametrize("algos", [[0, 2, 0, 2], [3, 3, 0, 0, 2], [0, 0, 3], [2, 0, 2, 3, 2], [3, 2, 2, 0]])
+@pytest.mark.parametrize("algos", [[0, 2, 0, 2], [4, 4, 0, 0, 2], [0, 0, 4], [2, 0, 2, 4, 2], [4, 2, 2, 0]])
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
 def test_sim_switching_schedules_on_one_communicator(oracle_lib, sim_lib, algos, n):
     # mncclCommSetAlgo between calls: per-pair FIFO counters keep every link consistent
@@ -116,7 +116,7 @@ def test_sim_oneshot(oracle_lib, sim_lib, n, count, inplace):
     assert all(same_bits(g, e) for g, e in zip(got, ref))
 
 
-@pytest.mark.parametrize("algos", [[1, 0, 1, 2], [3, 1, 1, 0, 2], [0, 0, 1], [2, 1, 2, 3, 1], [1, 2, 2, 0, 1, 1]])
+@pytest.mark.parametrize("algos", [[1, 0, 1, 2], [4, 1, 1, 0, 2], [0, 0, 1], [2, 1, 2, 4, 1], [1, 2, 2, 0, 1, 1]])
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
 def test_sim_oneshot_switching_schedules(oracle_lib, sim_lib, algos, n):
     # the one-shot shares the per-(pair, pipeline) FIFO counters, READY words, credits and slots
@@ -163,7 +163,7 @@ def test_effective_slice_properties(sim_lib, chunk, C):
     assert S.effective_slice(chunk, C, slice_bytes, slice_bytes) == slice_bytes  # MIN_SLICE >= SLICE: off
 
 
-@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_LOAD], ids=["ring", "read", "read_load"])
+@pytest.mark.parametrize("algo", [S.RING, S.READ, S.READ_GRID], ids=["ring", "read", "read_grid"])
 @pytest.mark.parametrize("n,count,seed", [(2, 70001, 1), (3, 40000, 2), (4, 9000, 3), (8, 123457, 4)])
 def test_sim_adaptive_slice(oracle_lib, sim_lib, algo, n, count, seed):
     # payload shrunk below the slot stride, random interleavings over 3 calls: same bits
@@ -185,7 +185,7 @@ def test_sim_ring_partial_grid_random_interleavings(oracle_lib, sim_lib, n, seed
     for i, count in enumerate(sizes):
         xs = O.random_inputs(n, count, "f32", seed=100 * seed + i)
         ref = O.allreduce(xs, slice_bytes=64)
-        algos = [S.RING, S.RING, S.READ if i % 2 else S.READ_LOAD, S.RING]
+        algos = [S.RING, S.RING, S.READ if i % 2 else S.READ_GRID, S.RING]
         got, _ = S.allreduce(xs, slice_bytes=64, channels=C, slots=2, algos=algos, seed=seed + i)
         assert all(same_bits(g, e) for g, e in zip(got, ref)), (count, algos)
 
@@ -211,12 +211,12 @@ def test_call_pipelines(sim_lib, nslices, C, waves, want):
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
 @pytest.mark.parametrize("seed", range(1, 7))
 def test_sim_read_in_place_random_interleavings(oracle_lib, sim_lib, n, seed):
-    # the read schedule in place (send == recv): a rank overwrites its chunk q only after q's
-    # READY for that slice, i.e. after q has loaded its raw input from it; under random
-    # interleavings any earlier write would leave a wrong value behind
+    # the read schedule in place (send == recv): only rank c writes chunk c of any recv, after its
+    # own loads of that slice; under random interleavings any other order would leave a wrong
+    # value behind
     xs = O.random_inputs(n, 3000 + 7 * seed, "f32", seed=seed)
     ref = O.allreduce(xs, slice_bytes=64)
-    for algo in (S.READ, S.READ_LOAD):
+    for algo in (S.READ, S.READ_GRID):
         got, _ = S.allreduce(xs, algo=algo, slice_bytes=64, channels=1 + seed % 4, calls=1, seed=seed, inplace=True)
         assert all(same_bits(g, e) for g, e in zip(got, ref)), algo
 
@@ -229,16 +229,15 @@ def test_sim_read_needs_no_slots(oracle_lib, sim_lib):
 
 
 def test_read_message_counts(sim_lib):
-    # per pipeline and call: START (publish + wait), one fold-and-push per iteration (push form:
-    # no READY, no copies), DONE (publish + wait); load form: per iteration one fold (+ READY)
-    # and n-1 copies, one extra step to leave the loop
+    # per pipeline and call: START (publish + wait), one fold-and-push per iteration (no READY,
+    # no copies), DONE (publish + wait); the 4.0-5.x load form (schedule code 3) is refused
     n, C = 4, 2
     xs = O.random_inputs(n, n * 64, "f32")
     _, steps = S.allreduce(xs, algo=S.READ, slice_bytes=64, channels=C)
     iters = -(-(64 * 4 // 64) // C)
     assert steps == n * C * (4 + iters)
-    _, steps = S.allreduce(xs, algo=S.READ_LOAD, slice_bytes=64, channels=C)
-    assert steps == n * C * (4 + iters * n + 1)
+    with pytest.raises(ValueError):
+        S.allreduce(xs, algo=3, slice_bytes=64, channels=C)
 
 
 @pytest.mark.parametrize("chunk", [0, 4, 1000, 1 << 16, (1 << 20) + 12, 3 << 22, 1 << 27, 1 << 30])
@@ -268,7 +267,7 @@ def test_read_small_calls_run_only_the_pipelines_they_need(oracle_lib, sim_lib, 
     _, steps = S.allreduce(xs, algo=2, slice_bytes=64, channels=C)
     assert steps == n * 3 * (4 + 1)  # iters = 1 on 3 pipelines
     for seed in range(3):
-        got, _ = S.allreduce(xs, slice_bytes=64, channels=C, algos=[2, 0, 2, 3, 2, 2, 0, 3, 2], seed=seed + 1)
+        got, _ = S.allreduce(xs, slice_bytes=64, channels=C, algos=[2, 0, 2, 4, 2, 2, 0, 4, 2], seed=seed + 1)
         assert all(same_bits(g, e) for g, e in zip(got, ref))
 
 
@@ -332,23 +331,22 @@ def test_sim_registered_window_signatures_random_interleavings(sim_lib, n):
 
 
 def test_read_grid_form_rule(sim_lib):
-    # forced (mncclAlgoReadGrid) or auto: the push form's calls with chunks of >= 4 MiB in whole
-    # 16-byte vectors at 2-8 ranks take the grid form; the load form, unaligned calls, smaller
-    # chunks, more ranks and a forced persistent read (mncclAlgoRead) keep the persistent kernel
+    # forced (mncclAlgoReadGrid) or auto: calls with chunks of >= 4 MiB in whole 16-byte vectors
+    # at 2-8 ranks take the grid form; unaligned calls, smaller chunks, more ranks and a forced
+    # persistent read (mncclAlgoRead) keep the persistent kernel
     big = 4 << 20
     for n in (2, 3, 5, 8):
-        assert S.read_grid_form(True, False, True, True, big, n)
-        assert S.read_grid_form(False, True, True, True, big, n)
-        assert not S.read_grid_form(False, False, True, True, big, n)  # MINI_NCCL_ALGO=read
-        assert not S.read_grid_form(False, True, False, True, big, n)  # MINI_NCCL_READ_PUSH=0
-        assert not S.read_grid_form(False, True, True, False, big, n)  # element-wise path
-        assert not S.read_grid_form(False, True, True, True, big - 16, n)
-        assert not S.read_grid_form(False, True, True, True, big + 8, n)
-    assert not S.read_grid_form(True, True, True, True, big, 9)
-    assert not S.read_grid_form(True, True, True, True, big, 1)
+        assert S.read_grid_form(True, False, True, big, n)
+        assert S.read_grid_form(False, True, True, big, n)
+        assert not S.read_grid_form(False, False, True, big, n)  # MINI_NCCL_ALGO=read
+        assert not S.read_grid_form(False, True, False, big, n)  # element-wise path
+        assert not S.read_grid_form(False, True, True, big - 16, n)
+        assert not S.read_grid_form(False, True, True, big + 8, n)
+    assert not S.read_grid_form(True, True, True, big, 9)
+    assert not S.read_grid_form(True, True, True, big, 1)
     # MINI_NCCL_GRID_MIN moves the threshold (the node's sweep weighs DDP-bucket-sized calls)
-    assert S.read_grid_form(False, True, True, True, 256 << 10, 8, min_bytes=256 << 10)
-    assert not S.read_grid_form(False, True, True, True, (256 << 10) - 16, 8, min_bytes=256 << 10)
+    assert S.read_grid_form(False, True, True, 256 << 10, 8, min_bytes=256 << 10)
+    assert not S.read_grid_form(False, True, True, (256 << 10) - 16, 8, min_bytes=256 << 10)
 
 
 
@@ -360,7 +358,7 @@ def test_sim_grid_form_between_other_schedules(oracle_lib, sim_lib, n):
     # stay in step because every rank skips them alike)
     import oracle_api as O
     plans = [[S.READ_GRID, S.RING, S.READ_GRID, S.READ, S.ONESHOT, S.READ_GRID],
-             [S.READ, S.READ_GRID, S.READ_LOAD, S.READ_GRID, S.RING, S.READ]]
+             [S.READ, S.READ_GRID, S.RING, S.READ_GRID, S.READ, S.READ]]
     for i, algos in enumerate(plans):
         count = n * 700 + i
         xs = O.random_inputs(n, count, "f32", seed=60 + i)
