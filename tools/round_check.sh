@@ -1,25 +1,25 @@
 #!/bin/bash
-# Round-4 evidence on the one GPU, step by step (each under its own time limit; the first failure
-# ends the call): STEP=suite -> the whole -m gpu suite (one process) + smoke; STEP=n1 -> bench.py
-# N=1 and its rocprofv3 evidence (kernel trace + FETCH / WRITE passes); STEP=proxy -> the N > 1
+# A round's evidence on the one GPU, step by step (each under its own time limit; the first failure
+# ends the call): STEP=suite -> the whole -m gpu suite (one process) + smoke (PYTEST_K: a -k filter);
+# STEP=n1 -> bench.py N=1 and its rocprofv3 evidence from the same lease (tools/profile_n1.sh,
+# HEAD=<commit>); STEP=proxy -> the N > 1
 # bench flow with NRS rank processes sharing the GPU; STEP=small -> small calls by rank count;
 # STEP=stress -> the mixed-schedule stress at 8 and 3 ranks; STEP=inject -> the injected-abort
-# rehearsal.  Outputs under gpurun_out/<RND>_<step>/ (RND: r4 by default; round 5 runs RND=r5).
+# rehearsal.  Outputs under gpurun_out/<RND>_<step>/ (RND: r6 by default).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 for step in ${STEP:-suite}; do
-  O=gpurun_out/${RND:-r4}_$step; mkdir -p $O
+  O=gpurun_out/${RND:-r6}_$step; mkdir -p $O
   case $step in
     suite)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 10
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/gpu_tests.log 2>&1 || exit 10
       tail -2 $O/gpu_tests.log
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 11
       tail -2 $O/smoke.log ;;
     n1)
-      timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_n1.json 2> $O/bench_n1.err || exit 12
-      cut -c1-400 $O/bench_n1.json
-      bash tools/profile_n1.sh ${RND:-r4}_n1/prof || exit 13 ;;
+      bash tools/profile_n1.sh ${RND:-r6}_n1 ${HEAD:-unknown} || exit 13
+      cut -c1-400 gpurun_out/${RND:-r6}_n1/line_plain.json ;;
     proxy)
       for n in ${NRS:-2 4 8}; do
         GPU_MAX_HW_QUEUES=2 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
