@@ -103,6 +103,7 @@ struct PeerInfo {
   uint64_t scratch_ptr, mbox_ptr;  // raw addresses (same-process ranks) / the allocations' bases
   uint64_t scratch_id, mbox_id;    // HIP allocation ids (the import registry's keys)
   int64_t retired_mb;              // MINI_NCCL_RETIRED_MB as configured (-1: the default)
+  int32_t window_rendezvous, pad1; // MINI_NCCL_WINDOW_RENDEZVOUS as configured
 };
 constexpr uint32_t kInfoMagic = 0x4d4e4934u;  // 'MNI4' (4.0's record: a 3.x rank fails the check)
 
@@ -197,6 +198,7 @@ void Comm::exchange_and_map() {
   me.scratch_id = scratch_id_;
   me.mbox_id = mbox_id_;
   me.retired_mb = cfg_.retired_mb;
+  me.window_rendezvous = cfg_.window_rendezvous;
 
   std::vector<PeerInfo> all((size_t)nranks_);
   boot_.allgather(&me, all.data(), sizeof me);
@@ -209,14 +211,16 @@ void Comm::exchange_and_map() {
     if (p.slice != me.slice || p.channels != me.channels || p.slots != me.slots || p.threads != me.threads ||
         p.window != me.window || p.signal_batch != me.signal_batch || p.scratch_cap != me.scratch_cap ||
         p.algo != me.algo || p.abi != me.abi || p.grid_min_kib != me.grid_min_kib ||
-        p.retired_mb != me.retired_mb)
+        p.retired_mb != me.retired_mb || p.window_rendezvous != me.window_rendezvous)
       throw std::invalid_argument(
           "MINI_NCCL_SLICE_SIZE / WINDOW_SIZE / SIGNAL_BATCH / SLOTS / CHANNELS / THREADS / SCRATCH_MB / ALGO / "
-          "GRID_MIN / RETIRED_MB differ between ranks (or their library versions differ)");
+          "GRID_MIN / RETIRED_MB / WINDOW_RENDEZVOUS differ between ranks (or their library versions differ)");
   }
   ranks_on_device_ = 0;
   for (int q = 0; q < nranks_; ++q)
     if (all[(size_t)q].pci == me.pci) ++ranks_on_device_;
+  // window calls without a host rendezvous: the same answer on every rank (from the knob alone)
+  window_fast_ = cfg_.window_rendezvous != 1;
   // Rank PROCESSES sharing this GPU: a persistent kernel waits for its peers' kernels, so all of
   // them must be resident at once; the GPU's scheduler maps a bounded number of processes and
   // hardware queues together, beyond which it time-slices and every hand-off waits for a turn
@@ -661,7 +665,7 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
                             pbuf_.available();
     // registered windows: the read schedule with no host rendezvous (no record to wait for, no
     // pointer query) -- every rank promised the same windows and offsets, the kernel checks it
-    const Window* win_s = read_sched && !windows_.empty() ? find_window(send, bytes) : nullptr;
+    const Window* win_s = read_sched && window_fast_ && !windows_.empty() ? find_window(send, bytes) : nullptr;
     const Window* win_r = win_s ? find_window(recv, bytes) : nullptr;
     if (win_s && win_r) {
       const uint64_t os = (uint64_t)((const char*)send - win_s->base), orv = (uint64_t)((char*)recv - win_r->base);

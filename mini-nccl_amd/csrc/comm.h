@@ -114,6 +114,7 @@ class Comm {
   std::vector<Window> windows_;
   uint64_t next_window_ = 1;
   unsigned long long window_calls_ = 0;     // calls launched on registered windows (no rendezvous)
+  bool window_fast_ = true;                 // window calls skip the host rendezvous (MINI_NCCL_WINDOW_RENDEZVOUS)
   int ranks_on_device_ = 1;
   bool topo_read_ = true;        // auto may run the read schedule (every pair: same GPU or 1 xGMI hop)
   std::string topo_why_ = "read: one rank";

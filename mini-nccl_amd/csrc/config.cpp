@@ -106,6 +106,10 @@ Config Config::from_env() {
   c.grid_min = (size_t)gmin;
   if (c.grid_vectors != 0 && c.grid_vectors != 1 && c.grid_vectors != 2 && c.grid_vectors != 4)
     throw std::invalid_argument("MINI_NCCL_GRID_VECTORS=" + std::to_string(c.grid_vectors) + " (expected 0, 1, 2 or 4)");
+  c.window_rendezvous = (int)env_int("MINI_NCCL_WINDOW_RENDEZVOUS", -1);
+  if (c.window_rendezvous < -1 || c.window_rendezvous > 1)
+    throw std::invalid_argument("MINI_NCCL_WINDOW_RENDEZVOUS=" + std::to_string(c.window_rendezvous) +
+                                " (expected -1, 0 or 1)");
   c.retired_mb = env_int("MINI_NCCL_RETIRED_MB", -1);
   if (c.retired_mb < -1) c.retired_mb = -1;
   c.timeout_ms = (double)env_int("MINI_NCCL_TIMEOUT_MS", 10000);
@@ -120,10 +124,10 @@ std::string Config::describe() const {
   char b[320];
   snprintf(b, sizeof b,
            "SLICE_SIZE=%zu B, WINDOW=%d, BATCH=%d, slots=%d, channels=%d, threads=%d, scratch_cap=%zu MiB, algo=%s, "
-           "blocking=%d, sys_fence=%d, grid_vectors=%d, grid_min=%zu B, timeout=%.0f ms, port=%d",
+           "blocking=%d, sys_fence=%d, window_rendezvous=%d, grid_vectors=%d, grid_min=%zu B, timeout=%.0f ms, port=%d",
            slice_size, window_size, signal_batch, slots, channels, threads, scratch_cap >> 20,
            algo < 0 ? "auto" : algo == 2 ? "read" : algo == 3 ? "oneshot" : algo == 4 ? "read_grid" : "ring", blocking,
-           sys_fence, grid_vectors, grid_min, timeout_ms, port);
+           sys_fence, window_rendezvous, grid_vectors, grid_min, timeout_ms, port);
   return b;
 }
 

@@ -24,6 +24,10 @@ struct Config {
                                    // for fp32 Sum (a tuning knob for the node's sweep); 0 = schedule.h's rule
   size_t grid_min = 4u << 20;      // MINI_NCCL_GRID_MIN: the smallest chunk (bytes) a read call takes the grid
                                    // form for (schedule.h kReadGridMin; >= 64 KiB, 16-byte multiple; rank-uniform)
+  int window_rendezvous = -1;      // MINI_NCCL_WINDOW_RENDEZVOUS: calls on registered windows -- 0 launch with
+                                   // no host rendezvous (the signature checked on the device), 1 negotiate
+                                   // like other calls (the windows' buffers are mapped already), -1 auto
+                                   // (Comm::window_fast_; rank-uniform)
   long long retired_mb = -1;       // MINI_NCCL_RETIRED_MB: bytes of freed same-GPU peer allocations this process
                                    // may keep mapped (ipcreg.h close_import), in MiB; -1 = 1/8 of the GPU's
                                    // memory (Comm resolves it); past it, calls bringing a new same-GPU peer

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise an interleaved A/B log of tools/r4_read_ab.sh / r4_ring_small_ab.sh / r4_small_calls.sh
+"""Summarise an interleaved A/B log of tools/r4_read_ab.sh / r4_ring_small_ab.sh / small_calls.sh
 ("== <tag> round=R n=N ..." headers, perf_test rows "bytes us algbw busbw schedule"): per
 (ranks, bytes, tag) the us of every round, the median and the ratio to the first tag's median."""
 import collections
@@ -11,10 +11,10 @@ d = collections.defaultdict(list)
 tags = []
 tag = None
 for line in open(sys.argv[1]):
-    m = re.match(r"== (\S+) (?:round=\d+ )?n=(\d+)", line) or re.match(r"== n=(\d+) algo=(\S+) read_push=(\d)", line)
+    m = re.match(r"== (\S+) (?:round=\d+ )?n=(\d+)", line) or re.match(r"== n=(\d+) algo=(\S+)", line)
     if m:
         if line.startswith("== n="):
-            t, n = m.group(2) + ("" if m.group(3) == "1" or m.group(2) != "read" else "_load"), m.group(1)
+            t, n = m.group(2), m.group(1)
         else:
             t, n = m.group(1), m.group(2)
         tag = (t, int(n))

@@ -28,7 +28,7 @@ for step in ${STEP:-suite}; do
         echo "n=$n"; cut -c1-300 $O/bench_n${n}_same_gpu.json
       done ;;
     small)
-      ROUNDS="${ROUNDS:-1 2 3}" ITERS=500 timeout -k 10 600 bash tools/r4_small_calls.sh > $O/small_calls.txt 2>&1 || exit 30
+      ROUNDS="${ROUNDS:-1 2 3}" ITERS=500 timeout -k 10 600 bash tools/small_calls.sh > $O/small_calls.txt 2>&1 || exit 30
       python3 tools/ab_summary.py $O/small_calls.txt ;;
     stress)
       timeout -k 10 550 python -u tools/r4_stress_mixed.py --ranks 8 --calls 200 --seed 11 > $O/stress_n8.txt 2>&1 || exit 50
