@@ -540,9 +540,14 @@ def small_calls(M, torch, dist, comm, send, recv, stream, n, max_over_ranks, war
                     call()
                     torch.cuda.synchronize()
                 dt = max_over_ranks(time.perf_counter() - t0) / reps
-                ran = comm.info()["last_algo"]
-                if name == "read_window" and comm.info()["window_calls"] < warm + reps:
-                    ran = -1  # not the window path: reported as a failed point
+                ci = comm.info()
+                ran = ci["last_algo"]
+                if name == "read_window":
+                    # with no two ranks on one GPU window calls skip the host rendezvous; ranks sharing
+                    # a GPU negotiate them (MINI_NCCL_WINDOW_RENDEZVOUS auto: they meet faster on the host)
+                    row["read_window_path"] = "device" if ci["window_fast"] else "negotiated"
+                    if ci["window_fast"] and ci["window_calls"] < warm + reps:
+                        ran = -1  # not the window path: reported as a failed point
                 row[name + "_us"] = round(dt * 1e6, 1)
                 row[name + "_ok"] = max_over_ranks(0.0 if (ran == a and bool((r_ == float(n)).all().item()))
                                                    else 1.0) == 0.0

@@ -41,8 +41,9 @@ extern "C" {
    large read calls take the grid form wherever it fits (co-located ranks too);
    600 the read schedule's load form and MINI_NCCL_READ_PUSH removed (read_push is always 1), a
    byte budget on retired same-GPU imports (MINI_NCCL_RETIRED_MB; mncclCommInfo_t grew, same
-   prefix: retired_bytes, retired_budget, budget_refusals), window calls carry the launch form in
-   their signature */
+   prefix: retired_bytes, retired_budget, budget_refusals, window_fast), window calls carry the
+   schedule choice in their signature and skip the host rendezvous only when no two ranks share a
+   GPU (MINI_NCCL_WINDOW_RENDEZVOUS) */
 #define MNCCL_VERSION 600
 
 /* schedules; all produce bit-identical results (same fold order per element) */
@@ -149,6 +150,10 @@ typedef struct {
                                             (on every rank alike) */
   unsigned long long budget_refusals;    /* process-wide: same-GPU imports refused by that budget (each
                                             such call ran the ring; warned once per process) */
+  int window_fast;                       /* 1: calls on registered windows launch with no host
+                                            rendezvous (MINI_NCCL_WINDOW_RENDEZVOUS=0, or auto when
+                                            no two ranks share a GPU); 0: they are negotiated like
+                                            other calls (co-located ranks meet faster on the host) */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,
@@ -178,7 +183,9 @@ ncclResult_t mncclCommSetAlgo(ncclComm_t comm, int algo);
  * overwrites scratch slots). */
 ncclResult_t mncclCommLinkProbe(ncclComm_t comm, int allPeers, size_t bytes, int iters, double* gbps);
 
-/* Registered windows (since 500; NCCL's collective buffer registration).  COLLECTIVE: every rank
+/* Registered windows (since 500; NCCL's collective buffer registration; since 600 the no-rendezvous
+ * launch below applies when no two ranks share a GPU or with MINI_NCCL_WINDOW_RENDEZVOUS=0 --
+ * otherwise window calls are negotiated like any other, same results).  COLLECTIVE: every rank
  * calls mncclCommRegister with its buffer of the window -- device memory of its own GPU, the same
  * `size` on every rank -- in the same order (the window's number is the registration's).  After
  * it, an ncclAllReduce whose send and recv lie in registered windows -- the SAME windows at the

@@ -219,8 +219,16 @@ void Comm::exchange_and_map() {
   ranks_on_device_ = 0;
   for (int q = 0; q < nranks_; ++q)
     if (all[(size_t)q].pci == me.pci) ++ranks_on_device_;
-  // window calls without a host rendezvous: the same answer on every rank (from the knob alone)
-  window_fast_ = cfg_.window_rendezvous != 1;
+  // Window calls without a host rendezvous: by default only when no two ranks share a GPU.  Ranks
+  // sharing one GPU meet faster on the host than on the device -- 8 co-located ranks, 4 KiB blocking
+  // calls: 88 us per window call launched at once vs 68-70 us negotiated, 4 ranks 25.7 vs 24.8-25.2
+  // (profiles/r6_small_calls_windows.txt) -- since their kernels, launched out of step, spin for
+  // each other while 8 processes' dispatches share one command processor.  The same answer on
+  // every rank: every rank sees every PCI location.
+  bool shared_gpu = false;
+  for (int q = 0; q < nranks_; ++q)
+    for (int p = q + 1; p < nranks_; ++p) shared_gpu = shared_gpu || all[(size_t)q].pci == all[(size_t)p].pci;
+  window_fast_ = cfg_.window_rendezvous == 0 || (cfg_.window_rendezvous < 0 && !shared_gpu);
   // Rank PROCESSES sharing this GPU: a persistent kernel waits for its peers' kernels, so all of
   // them must be resident at once; the GPU's scheduler maps a bounded number of processes and
   // hardware queues together, beyond which it time-slices and every hand-off waits for a turn

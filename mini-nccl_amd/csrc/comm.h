@@ -49,6 +49,7 @@ class Comm {
   ncclResult_t deregister_window(void* handle);
   size_t windows() const { return windows_.size(); }
   unsigned long long window_calls() const { return window_calls_; }
+  bool window_fast() const { return window_fast_; }  // window calls skip the host rendezvous
   unsigned long long read_grid_calls() const { return read_grid_calls_; }  // calls run in the grid form
   size_t peer_mappings() const { return pbuf_.mapped_allocations(); }
   const PeerBuffers& peer_buffers() const { return pbuf_; }

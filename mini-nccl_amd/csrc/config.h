@@ -26,8 +26,8 @@ struct Config {
                                    // form for (schedule.h kReadGridMin; >= 64 KiB, 16-byte multiple; rank-uniform)
   int window_rendezvous = -1;      // MINI_NCCL_WINDOW_RENDEZVOUS: calls on registered windows -- 0 launch with
                                    // no host rendezvous (the signature checked on the device), 1 negotiate
-                                   // like other calls (the windows' buffers are mapped already), -1 auto
-                                   // (Comm::window_fast_; rank-uniform)
+                                   // like other calls (the windows' buffers are mapped already), -1 auto:
+                                   // 0 unless two ranks share a GPU (Comm::window_fast_; rank-uniform)
   long long retired_mb = -1;       // MINI_NCCL_RETIRED_MB: bytes of freed same-GPU peer allocations this process
                                    // may keep mapped (ipcreg.h close_import), in MiB; -1 = 1/8 of the GPU's
                                    // memory (Comm resolves it); past it, calls bringing a new same-GPU peer

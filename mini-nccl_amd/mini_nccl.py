@@ -64,7 +64,7 @@ class CommInfo(ctypes.Structure):
         ("retired_imports", ctypes.c_int),
         # since mncclVersion 600
         ("retired_bytes", ctypes.c_ulonglong), ("retired_budget", ctypes.c_ulonglong),
-        ("budget_refusals", ctypes.c_ulonglong),
+        ("budget_refusals", ctypes.c_ulonglong), ("window_fast", ctypes.c_int),
     ]
 
 

@@ -79,8 +79,10 @@ class TestLocalReduce:
 
 def _run_allreduce(n, cases, env=None, timeout=300, barrier=True):
     port = GW.free_port()
-    # every case sets its schedule explicitly; the ranks line up before each call (barrier)
-    e = {"MINI_NCCL_TIMEOUT_MS": "30000"}
+    # every case sets its schedule explicitly; the ranks line up before each call (barrier); window
+    # cases launch with no host rendezvous wherever the ranks are (the device-checked path; auto
+    # negotiates them when ranks share a GPU: test_registered_windows_auto_rendezvous)
+    e = {"MINI_NCCL_TIMEOUT_MS": "30000", "MINI_NCCL_WINDOW_RENDEZVOUS": "0"}
     e.update(env or {})
     out = GW.run_ranks(GW.allreduce_rank, n, lambda r: (r, n, port, cases, e), timeout,
                        barrier=barrier)
@@ -387,7 +389,7 @@ def test_read_grid_skewed_and_interleaved(dev):
 
 def _run_windows(n, scenario, env=None, timeout=300):
     port = GW.free_port()
-    e = {"MINI_NCCL_TIMEOUT_MS": "20000", **(env or {})}
+    e = {"MINI_NCCL_TIMEOUT_MS": "20000", "MINI_NCCL_WINDOW_RENDEZVOUS": "0", **(env or {})}
     out = GW.run_ranks(GW.window_rank, n, lambda r: (r, n, port, e, scenario), timeout, barrier=True)
     assert sorted(out) == list(range(n)), out
     for r in range(n):
@@ -409,6 +411,21 @@ def test_registered_windows_parity(dev, n):
         assert o["kinds"] == [2] * len(o["kinds"]), o["kinds"]  # the read schedule, every window call
         assert o["wc"] == [1] * len(o["wc"]), o["wc"]           # ... each without a rendezvous
         assert o["info"]["read_map_failures"] == 0 and o["info"]["ipc_open_failures"] == 0
+
+
+def test_registered_windows_auto_rendezvous(dev):
+    # MINI_NCCL_WINDOW_RENDEZVOUS unset (auto): window calls skip the host rendezvous only when no
+    # two ranks share a GPU; co-located ranks negotiate them like any other call (they meet faster
+    # on the host: profiles/r6_small_calls_windows.txt) -- the same bits either way
+    n = 3
+    out = _run_windows(n, "parity", {"MINI_NCCL_WINDOW_RENDEZVOUS": "-1"}, timeout=600)
+    shared = any(out[r]["info"]["ranks_on_device"] > 1 for r in range(n))
+    for r in range(n):
+        o = out[r]
+        assert all(rc == 0 for rc in o["rcs"]) and all(b == 0 for b in o["bad"]), (r, o["rcs"], o["bad"])
+        assert o["kinds"] == [2] * len(o["kinds"]), o["kinds"]
+        assert o["info"]["window_fast"] == (0 if shared else 1), o["info"]["window_fast"]
+        assert o["wc"] == [0 if shared else 1] * len(o["wc"]), o["wc"]
 
 
 def test_registered_windows_host_independent(dev):
@@ -759,7 +776,7 @@ def test_allreduce_hip_graph_capture_and_replay(dev, algo):
     if algo == "read_grid":
         env["GRAPH_COUNT"] = str(3 * (1 << 20) + 1)
     if algo == "read_window":  # registered windows: the captured launch carries its START signature
-        env["GRAPH_WINDOW"] = "1"
+        env.update(GRAPH_WINDOW="1", MINI_NCCL_WINDOW_RENDEZVOUS="0")
     out = GW.run_ranks(GW.graph_rank, 3, lambda r: (r, 3, port, env, 4), 240)
     assert sorted(out) == [0, 1, 2], out
     for r in range(3):
