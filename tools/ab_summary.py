@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise an interleaved A/B log of tools/r4_read_ab.sh / r4_ring_small_ab.sh / small_calls.sh
+"""Summarise an interleaved A/B log of tools/small_calls.sh / ab_perf_test.sh
 ("== <tag> round=R n=N ..." headers, perf_test rows "bytes us algbw busbw schedule"): per
 (ranks, bytes, tag) the us of every round, the median and the ratio to the first tag's median."""
 import collections

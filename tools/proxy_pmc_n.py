@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""PMC passes of tools/historical/r2_investigate.sh or tools/r2_profile_read.sh (gpurun_out/<tag>/{fetch,write}_<form>_n<N>) -> per-launch
+"""PMC passes of tools/profile_proxy_kernels.sh (gpurun_out/<tag>/{fetch,write}_<form>_n<N>) -> per-launch
 HBM bytes of rank 0's kernel on the N-rank one-GPU proxy, with the gfx950 corrections (FETCH x2,
 KiB x1024, MI355X_MICROARCH.md), against the fused algorithmic bytes of its kernel form (bench.py
-fused_bytes: ring (6n-4) chunks, read_push 2n, read_load 3n-1), next to the kernel-trace durations.
+fused_bytes: ring (6n-4) chunks, read_push / read_grid 2n), next to the kernel-trace durations.
 
-  python tools/proxy_pmc_n.py <tag> <round> <n> ring read_push read_load ...
+  python tools/proxy_pmc_n.py <tag> <round> <n> ring read_push read_grid ...
       -> profiles/<round>_proxy_pmc_n<N>.csv, profiles/<round>_proxy_kernel_stats_n<N>.csv,
          and the "<form>_f32_1GiB_n<N>_same_gpu" entries of profiles/pmc_summary.json, each
          carrying its kernel_form (bench.py refuses an entry of another form)
@@ -40,7 +40,7 @@ def main():
     algos = sys.argv[4:] or ["ring", "read_push"]
     base = os.path.join(ROOT, "gpurun_out", tag)
     def fused_of(form):  # bench.py fused_bytes
-        return 4 * (COUNT // n) * {"ring": 6 * n - 4, "read_push": 2 * n, "read_grid": 2 * n, "read_load": 3 * n - 1}[form]
+        return 4 * (COUNT // n) * {"ring": 6 * n - 4, "read_push": 2 * n, "read_grid": 2 * n}[form]
     summ_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     summ = json.load(open(summ_path)) if os.path.exists(summ_path) else {}
     pmc_csv = os.path.join(ROOT, "profiles", f"{rnd}_proxy_pmc_n{n}.csv")
@@ -52,10 +52,10 @@ def main():
                      "fused_alg_bytes", "fused_GBps_one_rank", "ranks_x_fused_GBps"])
         for algo in algos:
             fused = fused_of(algo)
-            # the kernel's template arguments name its form: read_kernel<float, 0, true, PUSH>
+            # the kernel's template arguments name its form: read_kernel<float, 0, true>
             # (the grid form: its fold grid, read_grid_kernel<float, 0, G, V>; START / DONE are one wave each)
-            k = {"ring": "ring_kernel<float, 0, true>", "read_push": "read_kernel<float, 0, true, true>",
-                 "read_grid": "read_grid_kernel<float, 0,", "read_load": "read_kernel<float, 0, true, false>"}[algo]
+            k = {"ring": "ring_kernel<float, 0, true>", "read_push": "read_kernel<float, 0, true>",
+                 "read_grid": "read_grid_kernel<float, 0,"}[algo]
             tr = rows(os.path.join(base, f"trace_{algo}_n{n}", "run_kernel_trace.csv"), k)
             durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr]
             md = med_after5(durs)

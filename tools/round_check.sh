@@ -31,11 +31,11 @@ for step in ${STEP:-suite}; do
       ROUNDS="${ROUNDS:-1 2 3}" ITERS=500 timeout -k 10 600 bash tools/small_calls.sh > $O/small_calls.txt 2>&1 || exit 30
       python3 tools/ab_summary.py $O/small_calls.txt ;;
     stress)
-      timeout -k 10 550 python -u tools/r4_stress_mixed.py --ranks 8 --calls 200 --seed 11 > $O/stress_n8.txt 2>&1 || exit 50
-      timeout -k 10 400 python -u tools/r4_stress_mixed.py --ranks 3 --calls 200 --seed 12 > $O/stress_n3.txt 2>&1 || exit 51
+      timeout -k 10 550 python -u tools/stress_mixed.py --ranks 8 --calls 200 --seed 11 > $O/stress_n8.txt 2>&1 || exit 50
+      timeout -k 10 400 python -u tools/stress_mixed.py --ranks 3 --calls 200 --seed 12 > $O/stress_n3.txt 2>&1 || exit 51
       grep STRESS $O/stress_n8.txt $O/stress_n3.txt ;;
     inject)
-      timeout -k 10 1100 bash tools/r4_inject_check.sh > $O/inject_check.txt 2>&1 || exit 40
+      timeout -k 10 1100 bash tools/inject_check.sh > $O/inject_check.txt 2>&1 || exit 40
       tail -12 $O/inject_check.txt ;;
   esac
 done

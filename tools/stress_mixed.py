@@ -11,7 +11,7 @@ counted and its case runs unregistered.  Schedules share the per-pair FIFO count
 READY words, credits and slots; any protocol slip shows as a wrong result, a hang (watchdog) or
 an error.  One summary line per rank and a verdict.
 
-    python tools/r4_stress_mixed.py [--ranks 8] [--calls 300] [--seed 11]
+    python tools/stress_mixed.py [--ranks 8] [--calls 300] [--seed 11]
 """
 import argparse
 import collections
