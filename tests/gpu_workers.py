@@ -597,7 +597,9 @@ def init_rank(rank, n, port, env, out_q):
 def mismatch_rank(rank, n, port, env, out_q):
     """Read schedule: ranks pass different counts to one call (a caller bug the reference would
     hang or corrupt on) -> every rank gets ncclInvalidUsage from the per-call rendezvous, and the
-    communicator stays usable: a matching call right after is bit-exact."""
+    communicator stays usable: a matching call right after is bit-exact.  MISMATCH=algo: the
+    counts agree but rank 0 chose auto and the others mncclAlgoRead (mncclCommSetAlgo is per rank:
+    auto would launch the grid form, read the persistent kernel) -- the same ncclInvalidUsage."""
     try:
         os.environ.update(env)
         os.environ["MINI_NCCL_PORT"] = str(port)
@@ -611,7 +613,12 @@ def mismatch_rank(rank, n, port, env, out_q):
         xs = O.random_inputs(n, count, "f32", seed=321)
         send, recv = hip_rt.DeviceBuffer(count * 4), hip_rt.DeviceBuffer(count * 4)
         send.upload(xs[rank])
-        rc_bad = comm.all_reduce(send.ptr, recv.ptr, count - rank, M.ncclFloat, M.ncclSum, st.handle)
+        if os.environ.get("MISMATCH") == "algo":
+            comm.set_algo(M.ALGO_AUTO if rank == 0 else M.ALGO_READ)
+            rc_bad = comm.all_reduce(send.ptr, recv.ptr, count, M.ncclFloat, M.ncclSum, st.handle)
+            comm.set_algo(M.ALGO_READ)
+        else:
+            rc_bad = comm.all_reduce(send.ptr, recv.ptr, count - rank, M.ncclFloat, M.ncclSum, st.handle)
         rc_ok = comm.all_reduce(send.ptr, recv.ptr, count, M.ncclFloat, M.ncclSum, st.handle)
         st.sync()
         got = recv.download(np.float32, count)
@@ -902,6 +909,8 @@ def window_rank(rank, n, port, env, scenario, out_q, barrier=None):
       async    -- MINI_NCCL_BLOCKING=0, rank 1 sleeps 50 ms before each call: rank 0's call returns
                   without waiting for it (host time reported), results bit-exact
       mismatch -- rank 0 passes another offset: every rank's call fails with ncclInvalidUsage
+      mismatch_algo -- same windows and offsets, but rank 0 chose auto and the others mncclAlgoRead
+                  (different kernel forms for a large call): the same ncclInvalidUsage
       unregistered -- rank 0 passes window buffers, the others buffers outside any window: every
                   rank fails fast (no watchdog wait)"""
     try:
@@ -972,7 +981,7 @@ def window_rank(rank, n, port, env, scenario, out_q, barrier=None):
                 st.sync()
                 bad.append(-1 if rc else compare(rbuf.download(np.float32, count), O.allreduce(xs)[rank], "f32", True)[0])
             res.update(call_s=times, bad=bad, window_calls=comm.info()["window_calls"])
-        elif scenario in ("mismatch", "unregistered"):
+        elif scenario in ("mismatch", "mismatch_algo", "unregistered"):
             count = 100003
             other = hip_rt.DeviceBuffer(count * 4)
             barrier.wait(120)
@@ -980,6 +989,9 @@ def window_rank(rank, n, port, env, scenario, out_q, barrier=None):
             if scenario == "mismatch":
                 off = 4096 if rank == 0 else 0
                 rc = comm.all_reduce(sbuf.ptr + off, rbuf.ptr + off, count, M.ncclFloat, M.ncclSum, st.handle)
+            elif scenario == "mismatch_algo":
+                comm.set_algo(M.ALGO_AUTO if rank == 0 else M.ALGO_READ)
+                rc = comm.all_reduce(sbuf.ptr, rbuf.ptr, n << 20, M.ncclFloat, M.ncclSum, st.handle)  # 4 MiB chunks: auto would take the grid form
             else:
                 p = sbuf.ptr if rank == 0 else other.ptr
                 rc = comm.all_reduce(p, p, count, M.ncclFloat, M.ncclSum, st.handle)

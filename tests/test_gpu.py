@@ -440,11 +440,13 @@ def test_registered_windows_host_independent(dev):
     assert max(o0["call_s"]) < 0.01, o0["call_s"]  # far below the 50 ms a rendezvous would wait
 
 
-def test_registered_windows_mismatch_is_invalid_usage(dev):
-    # a window call whose ranks pass different offsets: the kernels see the signatures differ at
-    # START and give up before touching a buffer -- ncclInvalidUsage on every rank, sticky
+@pytest.mark.parametrize("scenario", ["mismatch", "mismatch_algo"])
+def test_registered_windows_mismatch_is_invalid_usage(dev, scenario):
+    # a window call whose ranks pass different offsets (or, ADVICE r5, made different schedule
+    # choices: auto's grid form against a forced persistent read): the kernels see the signatures
+    # differ at START and give up before touching a buffer -- ncclInvalidUsage on every rank, sticky
     import mini_nccl as M
-    out = _run_windows(3, "mismatch")
+    out = _run_windows(3, scenario)
     for r in range(3):
         o = out[r]
         assert o["rc"] == M.ncclInvalidUsage and o["rc2"] == M.ncclInvalidUsage, (r, o)
@@ -489,12 +491,14 @@ def test_oneshot_host_buffers(dev, mem):
     _run_allreduce(3, cases)
 
 
-def test_read_schedule_count_mismatch_is_invalid_usage(dev):
-    # MINI_NCCL_ALGO=read: every rank sees every rank's (count, dtype, op) in the per-call
-    # rendezvous, so a call whose ranks disagree fails on all of them alike, and nothing is left
-    # half-done: the next (matching) call is bit-exact
+@pytest.mark.parametrize("what", ["count", "algo"])
+def test_read_schedule_count_mismatch_is_invalid_usage(dev, what):
+    # MINI_NCCL_ALGO=read: every rank sees every rank's (count, dtype, op, schedule choice) in the
+    # per-call rendezvous, so a call whose ranks disagree fails on all of them alike, and nothing is
+    # left half-done: the next (matching) call is bit-exact.  "algo": one rank on auto, the others
+    # on mncclAlgoRead (they would launch different kernel forms)
     port = GW.free_port()
-    env = {"MINI_NCCL_ALGO": "read", "MINI_NCCL_TIMEOUT_MS": "20000"}
+    env = {"MINI_NCCL_ALGO": "read", "MINI_NCCL_TIMEOUT_MS": "20000", "MISMATCH": what}
     out = GW.run_ranks(GW.mismatch_rank, 3, lambda r: (r, 3, port, env), 180)
     for r in range(3):
         assert "error" not in out[r], out[r].get("error")
