@@ -45,7 +45,8 @@ def main():
                           fresh=bool(mem == "device" and rng.random() < 0.2), skew_ms=3,
                           window=bool(mem == "device" and rng.random() < 0.25), window_optional=True))
     port = GW.free_port()
-    env = {"MINI_NCCL_TIMEOUT_MS": "30000", "GPU_MAX_HW_QUEUES": "2"}
+    # window calls on the device-checked path (auto would negotiate them: the ranks share a GPU)
+    env = {"MINI_NCCL_TIMEOUT_MS": "30000", "GPU_MAX_HW_QUEUES": "2", "MINI_NCCL_WINDOW_RENDEZVOUS": "0"}
     out = GW.run_ranks(GW.allreduce_rank, n, lambda r: (r, n, port, cases, env), 2400, barrier=True)
     ok = len(out) == n
     names = {0: "ring", 2: "read", 3: "oneshot", -1: "none"}
