@@ -654,6 +654,17 @@ __device__ __forceinline__ void read_fold_wide(const CollParams& p, uint64_t cof
 // owner's memory, which drops any copy of the line the owner's L2 kept (file header), and this
 // rank never reads the pushed ranges inside the call.
 
+// The fold's store into this rank's OWN recv: no peer reads it inside the call (the pushes are the
+// peers' copies), so it needs no system-scope write-through -- MNCCL_OWN_NT=1 stores it
+// non-temporal, as the local reduce does (an A/B knob; the pushes stay sc0 sc1).
+#ifndef MNCCL_OWN_NT
+#define MNCCL_OWN_NT 0
+#endif
+__device__ __forceinline__ void st_own16(rsrc_t r, uint32_t off, v4u v) {
+  if (MNCCL_OWN_NT) st_nt16(r, off, v);
+  else st_slot16(r, off, v);
+}
+
 template <typename T, int OPC, int G, int V>
 __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff, uint32_t nvec, int lane) {
   constexpr uint32_t step = 64 * V;
@@ -688,7 +699,7 @@ __device__ __forceinline__ void read_fold_all(const CollParams& p, uint64_t coff
         for (int u = 0; u < V; ++u) a[u] = reduce16<T, OPC>(x[g][u], a[u]);
       }
 #pragma unroll
-    for (int u = 0; u < V; ++u) st_slot16(out, (b + (uint32_t)(u * 64 + lane)) * 16, a[u]);
+    for (int u = 0; u < V; ++u) st_own16(out, (b + (uint32_t)(u * 64 + lane)) * 16, a[u]);
 #pragma unroll
     for (int g = 0; g < G; ++g)
       if (g + 1 < n) {
@@ -925,7 +936,7 @@ __global__ void __launch_bounds__(64) read_grid_kernel(CollParams p) {
       for (int u = 0; u < V; ++u) a[u] = reduce16<T, OPC>(x[g][u], a[u]);
     }
 #pragma unroll
-  for (int u = 0; u < V; ++u) st_slot16(out, (uint32_t)(u * 64 + lane) * 16, a[u]);
+  for (int u = 0; u < V; ++u) st_own16(out, (uint32_t)(u * 64 + lane) * 16, a[u]);
 #pragma unroll
   for (int g = 0; g < G; ++g)
     if (g + 1 < n) {
