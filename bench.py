@@ -262,7 +262,7 @@ def sweep_point(M, torch, dist, dev, n, rank, env, algo, count, reps, max_over_r
         ok = ok and i["last_algo"] == want
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
         return {"GBps": round(count * esz / (dt / reps) / 1e9, 2), "ok": ok, "workgroups": i["channels"],
-                "pipelines": i["pipelines"], "slot_bytes": i["slot_bytes"], "scratch_MiB": i["scratch_bytes"] >> 20,
+                "pipelines": i["pipelines"], "run_pipelines": i["run_pipelines"], "slot_bytes": i["slot_bytes"], "scratch_MiB": i["scratch_bytes"] >> 20,
                 "grid_calls": i["read_grid_calls"] - grid0}
     except Exception as e:
         return {"error": str(e)[:120]}
@@ -1207,7 +1207,8 @@ def main():
                                        f"rank, HIP IPC over xGMI, {algo} schedule",
                            "count": count, "bytes": nbytes, "algo": algo, "slice_bytes": info["slice_bytes"],
                            "channels": info["channels"], "slots": info["slots"], "threads": info["threads"],
-                           "pipelines": info["pipelines"], "scratch_bytes": info["scratch_bytes"],
+                           "pipelines": info["pipelines"], "run_pipelines": info["run_pipelines"],
+                           "scratch_bytes": info["scratch_bytes"],
                            "ranks_on_device": info["ranks_on_device"],
                            "parallelism": f"dp{n}", "result_check": "ok" if ok else "FAILED",
                            "headline_schedule": headline_why,

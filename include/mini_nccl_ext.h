@@ -41,7 +41,7 @@ extern "C" {
    large read calls take the grid form wherever it fits (co-located ranks too);
    600 the read schedule's load form and MINI_NCCL_READ_PUSH removed (read_push is always 1), a
    byte budget on retired same-GPU imports (MINI_NCCL_RETIRED_MB; mncclCommInfo_t grew, same
-   prefix: retired_bytes, retired_budget, budget_refusals, window_fast), window calls carry the
+   prefix: retired_bytes, retired_budget, budget_refusals, window_fast, run_pipelines), window calls carry the
    schedule choice in their signature and skip the host rendezvous only when no two ranks share a
    GPU (MINI_NCCL_WINDOW_RENDEZVOUS) */
 #define MNCCL_VERSION 600
@@ -154,6 +154,10 @@ typedef struct {
                                             rendezvous (MINI_NCCL_WINDOW_RENDEZVOUS=0, or auto when
                                             no two ranks share a GPU); 0: they are negotiated like
                                             other calls (co-located ranks meet faster on the host) */
+  int run_pipelines;                     /* the pipelines a call may launch: `pipelines`, capped so
+                                            that the waves of every rank sharing a GPU stay resident
+                                            together (CUs x 4 SIMDs x 2 waves / ranks on the most
+                                            crowded GPU) */
 } mncclCommInfo_t;
 
 ncclResult_t mncclLocalReduce(void* out, const void* local, const void* incoming, size_t count,

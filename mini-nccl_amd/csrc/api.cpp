@@ -201,6 +201,7 @@ ncclResult_t mncclCommGetInfoV(ncclComm_t comm, void* out, size_t size) {
   info->retired_budget = mnccl::ipc::retired_budget();
   info->budget_refusals = mnccl::ipc::budget_refusals();
   info->window_fast = c->window_fast() ? 1 : 0;
+  info->run_pipelines = c->run_pipes();
   memcpy(out, &full, size < sizeof full ? size : sizeof full);
   return ncclSuccess;
 }

@@ -103,7 +103,7 @@ struct PeerInfo {
   uint64_t scratch_ptr, mbox_ptr;  // raw addresses (same-process ranks) / the allocations' bases
   uint64_t scratch_id, mbox_id;    // HIP allocation ids (the import registry's keys)
   int64_t retired_mb;              // MINI_NCCL_RETIRED_MB as configured (-1: the default)
-  int32_t window_rendezvous, pad1; // MINI_NCCL_WINDOW_RENDEZVOUS as configured
+  int32_t window_rendezvous, cus;  // MINI_NCCL_WINDOW_RENDEZVOUS as configured; the GPU's CUs
 };
 constexpr uint32_t kInfoMagic = 0x4d4e4934u;  // 'MNI4' (4.0's record: a 3.x rank fails the check)
 
@@ -199,6 +199,10 @@ void Comm::exchange_and_map() {
   me.mbox_id = mbox_id_;
   me.retired_mb = cfg_.retired_mb;
   me.window_rendezvous = cfg_.window_rendezvous;
+  if (hipDeviceGetAttribute(&me.cus, hipDeviceAttributeMultiprocessorCount, device_) != hipSuccess) {
+    (void)hipGetLastError();
+    me.cus = 256;
+  }
 
   std::vector<PeerInfo> all((size_t)nranks_);
   boot_.allgather(&me, all.data(), sizeof me);
@@ -219,6 +223,26 @@ void Comm::exchange_and_map() {
   ranks_on_device_ = 0;
   for (int q = 0; q < nranks_; ++q)
     if (all[(size_t)q].pci == me.pci) ++ranks_on_device_;
+  // Residency: pipeline w of every rank waits for pipeline w of its peers, so the waves a call
+  // launches on the most crowded GPU must all be resident at once -- CUs x 4 SIMDs x
+  // kMinWavesPerSimd of them, shared by the ranks on that GPU.  A call launches at most run_pipes_
+  // pipelines (the mailbox / scratch / counter layout keeps all P; the others sit the call out, on
+  // every rank alike: the records are the same everywhere).  8 co-located ranks with
+  // MINI_NCCL_CHANNELS=512 (8 x 512 waves for 2048 slots) timed out without it.
+  {
+    int cus = 1 << 30, most = 1;
+    for (int q = 0; q < nranks_; ++q) {
+      cus = std::min(cus, std::max(1, (int)all[(size_t)q].cus));
+      int same = 0;
+      for (int p = 0; p < nranks_; ++p) same += all[(size_t)p].pci == all[(size_t)q].pci;
+      most = std::max(most, same);
+    }
+    const int w = geo_.waves, cap = std::max(w, cus * 4 * kMinWavesPerSimd / most / w * w);
+    run_pipes_ = std::min(wave_channels(), cap);
+    if (run_pipes_ < wave_channels() && rank_ == 0)
+      fprintf(stderr, "[Mini-NCCL] %d rank(s) share a GPU of %d CUs: calls launch at most %d of the communicator's %d "
+              "pipelines, so every rank's waves stay resident together\n", most, cus, run_pipes_, wave_channels());
+  }
   // Window calls without a host rendezvous: by default only when no two ranks share a GPU.  Ranks
   // sharing one GPU meet faster on the host than on the device -- 8 co-located ranks, 4 KiB blocking
   // calls: 88 us per window call launched at once vs 68-70 us negotiated, 4 ranks 25.7 vs 24.8-25.2
@@ -562,7 +586,8 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   p.send = (const char*)send;
   p.recv = (char*)recv;
   p.chunk_bytes = chunk_bytes;
-  const int C = wave_channels();
+  // C: the pipelines this call may launch (run_pipes_, <= the layout's wave_channels())
+  const int C = run_pipes();
   p.slot_bytes = wave_slice();
   p.slice_bytes = algo == 2   ? read_slice(chunk_bytes, C, cfg_.slice_size, kMinSlice, kReadDepth)
                   : algo == 3 ? oneshot_slice(chunk_bytes, n, C, wave_slice())
@@ -572,14 +597,14 @@ void Comm::launch(int algo, const void* send, void* recv, size_t chunk_bytes, in
   // per slice of every chunk
   const int A = call_pipelines(algo == 3 ? p.nslices * (uint64_t)n : p.nslices, C, geo_.waves);
   p.iters = (uint32_t)((p.nslices + (uint64_t)A - 1) / (uint64_t)A);
-  p.pipes = C;
+  p.pipes = wave_channels();
   p.n = n;
   p.rank = rank_;
   p.nslots = cfg_.slots;
   p.scratch = scratch_;
   p.mbox = mbox_;
   p.tx_seq = pair_seq_;
-  p.rx_seq = pair_seq_ + (size_t)n * C;
+  p.rx_seq = pair_seq_ + (size_t)n * wave_channels();
   for (int q = 0; q < n; ++q) {
     p.peer_scratch[q] = peer_scratch_[(size_t)q];
     p.peer_mbox[q] = peer_mbox_[(size_t)q];
@@ -664,8 +689,8 @@ ncclResult_t Comm::allreduce(const void* send, void* recv, size_t count, int dty
     // still wins at 8 ranks, profiles/r4_small_calls.txt, so auto keeps read first).  A pure
     // function of the call's size and the rank-uniform config up to the read rendezvous, which
     // all ranks decide alike.
-    const bool oneshot = algo_ == 3 && oneshot_fits(chunk_bytes, n, wave_channels(), wave_slice(), true);
-    const bool small = auto_ && oneshot_fits(chunk_bytes, n, wave_channels(), wave_slice(), false);
+    const bool oneshot = algo_ == 3 && oneshot_fits(chunk_bytes, n, run_pipes(), wave_slice(), true);
+    const bool small = auto_ && oneshot_fits(chunk_bytes, n, run_pipes(), wave_slice(), false);
     // (auto, and a forced one-shot's larger calls, only where the topology allows the read
     // schedule: classify_topology; MINI_NCCL_ALGO=read forces it anywhere)
     const bool read_sched = !oneshot &&

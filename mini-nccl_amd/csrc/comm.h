@@ -72,6 +72,9 @@ class Comm {
   // slot_bytes (MINI_NCCL_SLICE_SIZE unless the scratch cap shrank it) per message
   int workgroups() const { return geo_.workgroups; }
   int wave_channels() const { return geo_.workgroups * geo_.waves; }
+  // the pipelines a call may launch: wave_channels(), capped so that every co-located rank's waves
+  // fit the GPU at once (exchange_and_map)
+  int run_pipes() const { return run_pipes_ > 0 ? run_pipes_ : wave_channels(); }
   uint64_t wave_slice() const { return geo_.slot_bytes; }
 
  private:
@@ -116,6 +119,7 @@ class Comm {
   uint64_t next_window_ = 1;
   unsigned long long window_calls_ = 0;     // calls launched on registered windows (no rendezvous)
   bool window_fast_ = true;                 // window calls skip the host rendezvous (MINI_NCCL_WINDOW_RENDEZVOUS)
+  int run_pipes_ = 0;                       // 0 until exchange_and_map: run_pipes()
   int ranks_on_device_ = 1;
   bool topo_read_ = true;        // auto may run the read schedule (every pair: same GPU or 1 xGMI hop)
   std::string topo_why_ = "read: one rank";

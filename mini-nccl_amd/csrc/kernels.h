@@ -47,6 +47,10 @@ struct CollParams {
 };
 
 constexpr int kMaxRanks = 16;
+// The persistent collective kernels are built for at least this many resident waves per SIMD
+// (__launch_bounds__: <= 256 registers per wave): a GPU keeps CUs x 4 SIMDs x this many of their
+// waves resident at once, and every rank's pipeline w waits for its peers' pipeline w.
+constexpr int kMinWavesPerSimd = 2;
 
 // Launchers return hipSuccess or the launch error; dtype/op must be supported
 // (checked by the caller).  vec = 16-byte path (all offsets 16-byte aligned).

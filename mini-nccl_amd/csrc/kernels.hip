@@ -482,8 +482,8 @@ __device__ __forceinline__ WaveId wave_id() {
 // resident at once: 8 ranks x 256 one-wave pipelines = 2 waves on each of the 1024 SIMDs.  The
 // collective kernels therefore ask for >= 2 waves per SIMD (<= 256 VGPRs + AGPRs per wave; a
 // read-kernel variant at 256 + 1 AGPR fitted only one, and 8 co-located ranks crawled until
-// their watchdogs fired).  With one rank per GPU this costs nothing.
-constexpr int kMinWavesPerSimd = 2;
+// their watchdogs fired).  With one rank per GPU this costs nothing.  (kernels.h
+// kMinWavesPerSimd; Comm caps a call's pipelines so that every rank's waves fit, Comm::run_pipes.)
 
 template <typename T, int OPC, bool VEC>
 __global__ void __launch_bounds__(kMaxThreads, kMinWavesPerSimd) ring_kernel(CollParams p) {

@@ -65,6 +65,7 @@ class CommInfo(ctypes.Structure):
         # since mncclVersion 600
         ("retired_bytes", ctypes.c_ulonglong), ("retired_budget", ctypes.c_ulonglong),
         ("budget_refusals", ctypes.c_ulonglong), ("window_fast", ctypes.c_int),
+        ("run_pipelines", ctypes.c_int),
     ]
 
 

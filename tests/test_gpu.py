@@ -605,6 +605,25 @@ def test_freed_peer_buffers_beyond_the_import_cap(dev):
         print(f"rank {r}: {i['retired_imports']} retired imports hold {i['retired_bytes'] >> 20} MiB")
 
 
+def test_more_pipelines_than_stay_resident(dev):
+    # every rank's pipeline w waits for its peers' pipeline w, so the waves one call launches on a
+    # GPU must all be resident: 8 co-located ranks x 512 channels = 4096 one-wave pipelines for 2048
+    # wave slots (256 CUs x 4 SIMDs x 2) timed out in the round-6 proxy sweep.  A call now launches
+    # at most run_pipelines (all 512 when every rank has its own GPU); read, ring and one-shot
+    # calls bit-exact
+    n = 8
+    cases = [_case(count=(64 << 20) // 4 + 5, algo=2, seed=930), _case(count=(64 << 20) // 4, algo=0, seed=931),
+             _case(count=(1 << 20) + 3, algo=2, seed=932, calls=2, vary=True), _case(count=n * 512, algo=3, seed=933),
+             _case(count=(16 << 20) // 4, algo=4, seed=934)]
+    out = _run_allreduce(n, cases, {"MINI_NCCL_CHANNELS": "512", "GPU_MAX_HW_QUEUES": "2"}, timeout=600)
+    most = max(out[r]["info"]["ranks_on_device"] for r in range(n))
+    for r in range(n):
+        i = out[r]["info"]
+        assert i["pipelines"] == 512 and i["run_pipelines"] * most <= 2048, (i["pipelines"], i["run_pipelines"], most)
+        if most == 1:
+            assert i["run_pipelines"] == 512
+
+
 def test_read_schedule_send_recv_in_one_allocation(dev):
     # out of place with send and recv two regions of ONE allocation on every rank: the owner's
     # descriptor datagram carries that allocation once, both mappings come from one import;
