@@ -237,8 +237,7 @@ void Comm::exchange_and_map() {
       for (int p = 0; p < nranks_; ++p) same += all[(size_t)p].pci == all[(size_t)q].pci;
       most = std::max(most, same);
     }
-    const int w = geo_.waves, cap = std::max(w, cus * 4 * kMinWavesPerSimd / most / w * w);
-    run_pipes_ = std::min(wave_channels(), cap);
+    run_pipes_ = resident_pipes(wave_channels(), geo_.waves, cus, most, kMinWavesPerSimd);
     if (run_pipes_ < wave_channels() && rank_ == 0)
       fprintf(stderr, "[Mini-NCCL] %d rank(s) share a GPU of %d CUs: calls launch at most %d of the communicator's %d "
               "pipelines, so every rank's waves stay resident together\n", most, cus, run_pipes_, wave_channels());

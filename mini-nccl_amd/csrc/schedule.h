@@ -282,6 +282,18 @@ MNCCL_HD int topology_blocks_read(int n, const int* link, const int* hops) {
   return 0;
 }
 
+// The pipelines a call may launch (Comm::run_pipes): pipeline w of every rank waits for pipeline w
+// of its peers, so the waves a call launches on the most crowded GPU -- `most` ranks on a GPU of
+// `cus` CUs, each CU's 4 SIMDs keeping `waves_per_simd` of the kernels' waves resident -- must all
+// fit at once: min(P, cus x 4 x waves_per_simd / most), whole workgroups of `waves`, at least one.
+MNCCL_HD int resident_pipes(int P, int waves, int cus, int most, int waves_per_simd) {
+  if (most < 1) most = 1;
+  if (waves < 1) waves = 1;
+  int cap = cus * 4 * waves_per_simd / most / waves * waves;
+  if (cap < waves) cap = waves;
+  return P < cap ? P : cap;
+}
+
 // Whether a read-schedule call launches in the grid form (kernels.hip read_start / read_grid /
 // read_done) rather than the persistent read_kernel: forced (mncclAlgoReadGrid) or under auto,
 // for the push form's calls that fit it.  Auto took the grid only with every rank on a GPU of its

@@ -268,6 +268,9 @@ uint64_t mnccl_read_slice(uint64_t chunk_bytes, int channels, uint64_t slice, ui
 }
 
 int mnccl_call_pipelines(uint64_t nslices, int channels, int waves) { return call_pipelines(nslices, channels, waves); }
+int mnccl_resident_pipes(int P, int waves, int cus, int most, int waves_per_simd) {
+  return resident_pipes(P, waves, cus, most, waves_per_simd);
+}
 
 // schedule.h topology_blocks_read over an n x n matrix (rank q's row: how q's GPU reaches p's)
 int mnccl_topology_blocks_read(int n, const int* link, const int* hops) { return topology_blocks_read(n, link, hops); }

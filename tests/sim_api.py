@@ -24,6 +24,7 @@ def load():
         L.mnccl_read_slice.argtypes = [u64, i, u64, u64, i]
         L.mnccl_read_slice.restype = u64
         L.mnccl_call_pipelines.argtypes = [u64, i, i]
+        L.mnccl_resident_pipes.argtypes = [i, i, i, i, i]
         L.mnccl_topology_blocks_read.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(i)]
         L.mnccl_read_grid_form.argtypes = [i, i, i, u64, i, u64]
         L.mnccl_sim_signed_read.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), i, u64, i, u64,
@@ -99,6 +100,11 @@ def oneshot_slice(chunk_bytes, n, channels, slot_bytes):
 
 def oneshot_fits(chunk_bytes, n, channels, slot_bytes, forced=False):
     return bool(load().mnccl_oneshot_fits(chunk_bytes, n, channels, slot_bytes, int(forced)))
+
+
+def resident_pipes(P, waves, cus, most, waves_per_simd=2):
+    """csrc/schedule.h resident_pipes: the pipelines a call may launch with `most` ranks on a GPU."""
+    return load().mnccl_resident_pipes(P, waves, cus, most, waves_per_simd)
 
 
 def call_pipelines(nslices, channels, waves=1):

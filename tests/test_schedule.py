@@ -368,3 +368,17 @@ def test_sim_grid_form_between_other_schedules(oracle_lib, sim_lib, n):
             body = (count // n) * n
             for r in range(n):
                 assert np.array_equal(got[r][:body].view(np.uint32), ref[r][:body].view(np.uint32)), (algos, seed, r)
+
+
+@pytest.mark.parametrize("P,waves,cus,most,want", [
+    (256, 1, 256, 1, 256), (256, 1, 256, 8, 256),     # the default geometry: 8 co-located ranks fill 2048 slots exactly
+    (512, 1, 256, 8, 256), (512, 1, 256, 1, 512),     # MINI_NCCL_CHANNELS=512: capped only when ranks share a GPU
+    (4096, 4, 256, 1, 2048), (1024, 4, 256, 3, 680),  # 4-wave workgroups: whole workgroups
+    (256, 1, 256, 16, 128), (8, 4, 1, 16, 4)])        # never below one workgroup
+def test_resident_pipes(sim_lib, P, waves, cus, most, want):
+    # csrc/schedule.h resident_pipes: the waves one call launches on the most crowded GPU all fit
+    # its cus x 4 SIMDs x 2 slots (every rank's pipeline w waits for its peers' pipeline w)
+    got = S.resident_pipes(P, waves, cus, most)
+    assert got == want
+    assert got % waves == 0 and got <= P
+    assert got * most <= max(cus * 4 * 2, waves * most)
