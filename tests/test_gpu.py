@@ -619,9 +619,11 @@ def test_more_pipelines_than_stay_resident(dev):
     most = max(out[r]["info"]["ranks_on_device"] for r in range(n))
     for r in range(n):
         i = out[r]["info"]
-        assert i["pipelines"] == 512 and i["run_pipelines"] * most <= 2048, (i["pipelines"], i["run_pipelines"], most)
+        # (512 workgroups, fewer where the scratch cap bounds them: 292 at 8 ranks)
+        assert 256 < i["pipelines"] <= 512 and i["run_pipelines"] <= i["pipelines"], i
+        assert i["run_pipelines"] * most <= 2048, (i["pipelines"], i["run_pipelines"], most)
         if most == 1:
-            assert i["run_pipelines"] == 512
+            assert i["run_pipelines"] == i["pipelines"]
 
 
 def test_read_schedule_send_recv_in_one_allocation(dev):
