@@ -145,7 +145,7 @@ typedef struct {
   /* since 600 */
   unsigned long long retired_bytes;      /* process-wide: bytes those retired imports keep mapped */
   unsigned long long retired_budget;     /* MINI_NCCL_RETIRED_MB in bytes (default: 1/8 of this GPU's
-                                            memory): once retired_bytes reaches it, a call that would
+                                            memory / the ranks on it): once retired_bytes reaches it, a call that would
                                             map a new buffer of a same-GPU peer runs the ring instead
                                             (on every rank alike) */
   unsigned long long budget_refusals;    /* process-wide: same-GPU imports refused by that budget (each

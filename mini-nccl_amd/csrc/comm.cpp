@@ -278,7 +278,8 @@ void Comm::exchange_and_map() {
               procs.size(), device_, queues);
   }
   // the bytes of freed same-GPU peer allocations this process may keep mapped (ipcreg.h
-  // close_import): MINI_NCCL_RETIRED_MB, by default 1/8 of this GPU's memory (36 GB on MI355X)
+  // close_import): MINI_NCCL_RETIRED_MB, by default 1/8 of this GPU's memory shared by the ranks on
+  // it (36 GB on MI355X between them: each co-located process pins memory of the same GPU)
   if (ranks_on_device_ > 1) {
     uint64_t budget = (uint64_t)cfg_.retired_mb << 20;
     if (cfg_.retired_mb < 0) {
@@ -287,7 +288,7 @@ void Comm::exchange_and_map() {
         (void)hipGetLastError();
         total = (size_t)288 << 30;
       }
-      budget = (uint64_t)total / 8;
+      budget = (uint64_t)total / 8 / (uint64_t)ranks_on_device_;
     }
     ipc::set_retired_budget(budget);
   }

@@ -30,7 +30,7 @@ struct Config {
                                    // 0 unless two ranks share a GPU (Comm::window_fast_; rank-uniform)
   long long retired_mb = -1;       // MINI_NCCL_RETIRED_MB: bytes of freed same-GPU peer allocations this process
                                    // may keep mapped (ipcreg.h close_import), in MiB; -1 = 1/8 of the GPU's
-                                   // memory (Comm resolves it); past it, calls bringing a new same-GPU peer
+                                   // memory / the ranks on it (Comm resolves it); past it, calls bringing a new same-GPU peer
                                    // buffer run the ring (rank-uniform)
   double timeout_ms = 10000.0;     // MINI_NCCL_TIMEOUT_MS (reference watchdog: 10 s)
   int port = 8888;                 // MINI_NCCL_PORT   bootstrap port (reference: 8888)
