@@ -909,13 +909,21 @@ __global__ void __launch_bounds__(64) read_start_kernel(CollParams p) {
 // one batch of V vectors per lane of my chunk: the peers' slices of it loaded together (G peer
 // slots, as read_fold_all), folded in ring order, stored into my recv and pushed into every
 // peer's recv (the push order rotated by workgroup so the workgroups' stores spread over the links)
+// MNCCL_GRID_WAVES: one-wave batches per workgroup (an A/B knob: fewer, larger workgroups for the
+// dispatcher; each wave still folds its own batch, wave w of workgroup b batch b * W + w)
+#ifndef MNCCL_GRID_WAVES
+#define MNCCL_GRID_WAVES 1
+#endif
+constexpr int kGridWaves = MNCCL_GRID_WAVES;
+
 template <typename T, int OPC, int G, int V>
-__global__ void __launch_bounds__(64) read_grid_kernel(CollParams p) {
+__global__ void __launch_bounds__(64 * kGridWaves) read_grid_kernel(CollParams p) {
   if (*p.go != p.call_seq) return;  // START failed: the peers' buffers are not ours to touch
   constexpr uint32_t B = 64u * 16u * V;
-  const uint64_t off = (uint64_t)blockIdx.x * B;
+  const uint32_t batch = blockIdx.x * (uint32_t)kGridWaves + (kGridWaves > 1 ? threadIdx.x / 64u : 0u);
+  const uint64_t off = (uint64_t)batch * B;
   if (off >= p.chunk_bytes) return;
-  const int n = p.n, r = p.rank, lane = threadIdx.x;
+  const int n = p.n, r = p.rank, lane = kGridWaves > 1 ? (int)(threadIdx.x % 64u) : (int)threadIdx.x;
   const uint32_t len = (uint32_t)(p.chunk_bytes - off < B ? p.chunk_bytes - off : B);
   const uint64_t coff = (uint64_t)r * p.chunk_bytes + off;
   const rsrc_t loc = make_rsrc(p.send + coff, len), out = make_rsrc(p.recv + coff, len);
@@ -940,7 +948,7 @@ __global__ void __launch_bounds__(64) read_grid_kernel(CollParams p) {
 #pragma unroll
   for (int g = 0; g < G; ++g)
     if (g + 1 < n) {
-      const int q = direct_peer(n, r, 1 + (int)((g + blockIdx.x) % (unsigned)(n - 1)));
+      const int q = direct_peer(n, r, 1 + (int)((g + batch) % (unsigned)(n - 1)));
       const rsrc_t po = make_rsrc(p.peer_recv[q] + coff, len);
 #pragma unroll
       for (int u = 0; u < V; ++u) st_slot16(po, (uint32_t)(u * 64 + lane) * 16, a[u]);
@@ -1299,8 +1307,10 @@ static hipError_t read_grid_for_t(int op, const CollParams& p, hipStream_t st, i
   // the rule's instantiations below hard-code V per rank count; a rule they do not match is
   // refused rather than launched with a grid sized for another V
   if (!tuned && V != (n <= 4 ? 1 : 2)) return hipErrorInvalidValue;
-  const unsigned blocks = (unsigned)((p.chunk_bytes + 1024u * V - 1) / (1024u * V));
-#define GRID_G(OPC, G, VV) hipLaunchKernelGGL((read_grid_kernel<T, OPC, G, VV>), dim3(blocks), dim3(64), 0, st, p)
+  const uint64_t per_block = 1024ull * (uint64_t)V * kGridWaves;
+  const unsigned blocks = (unsigned)((p.chunk_bytes + per_block - 1) / per_block);
+#define GRID_G(OPC, G, VV) \
+  hipLaunchKernelGGL((read_grid_kernel<T, OPC, G, VV>), dim3(blocks), dim3(64 * kGridWaves), 0, st, p)
   if constexpr (std::is_same<T, float>::value) {
     if (tuned) {
 #define GRID_V(VV)                                    if (n == 2) GRID_G(kSum, 1, VV);                    else if (n == 3) GRID_G(kSum, 2, VV);               else if (n <= 5) GRID_G(kSum, 4, VV);               else GRID_G(kSum, 7, VV);
