@@ -856,6 +856,30 @@ def launch_plan(gpus, world_env, visible, same_device):
     return "spawn", None
 
 
+def summarize_proxy(d, n, rc):
+    """proxy_allreduce's fields from the rank processes' line `d` (a --core-only N > 1 line): the
+    default schedule (config.algo) and the ring, each with ms per call, kernel ms, its fractions and
+    its checks; ok only if both ran, rank 0 exited 0 and every check passed."""
+    out = {"rc": rc}
+    if "error" in d or not d.get("schedules"):
+        out["error"] = (d.get("error") or "no line from rank 0")[:300]
+    algo = (d.get("config") or {}).get("algo")
+    for name, p in (d.get("schedules") or {}).items():
+        if "value" not in p:
+            out[name] = {"error": p.get("error")}
+            continue
+        rf = p.get("roofline") or {}
+        out["default" if name == algo else name] = {
+            "schedule": name, "GBps": p["value"], "ms_per_call": p["ms_per_step"], "kernel_ms": p.get("kernel_ms"),
+            "sum_frac": rf.get("frac"), "fused_frac": rf.get("fused_frac"),
+            "fused_frac_all_ranks": round(n * rf["fused_frac"], 4) if rf.get("fused_frac") is not None else None,
+            "result_check": p.get("result_check"),
+            "order_sensitive": (p.get("verify") or {}).get("order_sensitive")}
+    out["ok"] = bool(rc == 0 and "default" in out and "ring" in out and all(
+        out[k].get("result_check") == "ok" and out[k].get("order_sensitive") == "ok" for k in ("default", "ring")))
+    return out
+
+
 def proxy_allreduce(budget_s=150.0):
     """VERDICT r5 #4, an extra of the N = 1 run (never `value`): BASELINE.json configs[1]'s shape,
     2 rank processes on GPU 0 (all ranks on one GPU, as the reference's perf_test, perf_test.cpp:46),
@@ -871,32 +895,14 @@ def proxy_allreduce(budget_s=150.0):
     env.pop("MINI_NCCL_ALGO", None)
     out = {"what": "labelled proxy, never `value`: 2 rank processes sharing GPU 0 (BASELINE.json configs[1]'s size; "
                    "every 'link' is this GPU's HBM), 256 MiB fp32 per rank, SLICE 128 KiB, GPU_MAX_HW_QUEUES=2, "
-                   "5 + 20 blocking-free calls per schedule, ms and GB/s = max over ranks of the wall clock between "
+                   "5 + 20 stream-ordered calls per schedule, ms and GB/s = max over ranks of the wall clock between "
                    "barriers; fused_frac_all_ranks = both ranks' fused HBM bytes / rank kernel time / 8 TB/s"}
     try:
         rc, line = spawn_ranks(argv, n, env=env, timeout=budget_s)
-        out["rc"] = rc
-        d = json.loads(line) if line else {}
+        out.update(summarize_proxy(json.loads(line) if line else {}, n, rc))
     except Exception as e:
         out["error"] = str(e)[:200]
         return out
-    if "error" in d or not d.get("schedules"):
-        out["error"] = (d.get("error") or "no line from rank 0")[:300]
-    algo = (d.get("config") or {}).get("algo")
-    for name, p in (d.get("schedules") or {}).items():
-        if "value" not in p:
-            out[name] = {"error": p.get("error")}
-            continue
-        rf = p.get("roofline") or {}
-        out["default" if name == algo else name] = {
-            "schedule": name, "GBps": p["value"], "ms_per_call": p["ms_per_step"], "kernel_ms": p.get("kernel_ms"),
-            "sum_frac": rf.get("frac"), "fused_frac": rf.get("fused_frac"),
-            "fused_frac_all_ranks": round(n * rf["fused_frac"], 4) if rf.get("fused_frac") is not None else None,
-            "result_check": p.get("result_check"),
-            "order_sensitive": (p.get("verify") or {}).get("order_sensitive")}
-    out["ok"] = bool(out.get("rc") == 0 and all(
-        isinstance(v, dict) and v.get("result_check") == "ok" and v.get("order_sensitive") == "ok"
-        for k, v in out.items() if k in ("default", "ring")) and "default" in out and "ring" in out)
     out["wall_s"] = round(time.time() - t0, 1)
     return out
 

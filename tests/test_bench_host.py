@@ -251,3 +251,22 @@ def test_bench_gpus_n_without_enough_gpus_prints_one_error_line():
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["value"] == 0.0 and d["n_gpus"] == 4 and "GPU(s) visible" in d["error"]
+
+
+def test_summarize_proxy_line():
+    # proxy_allreduce's reading of the rank processes' --core-only line
+    sys.path.insert(0, ROOT)
+    import bench
+
+    def sched(v, ok="ok", order="ok"):
+        return {"value": v, "ms_per_step": 1.0, "kernel_ms": 0.9, "result_check": ok,
+                "roofline": {"frac": 0.2, "fused_frac": 0.35}, "verify": {"order_sensitive": order}}
+
+    line = {"config": {"algo": "read_grid"}, "schedules": {"ring": sched(800.0), "read_grid": sched(1400.0)}}
+    s = bench.summarize_proxy(line, 2, 0)
+    assert s["ok"] and s["default"]["schedule"] == "read_grid" and s["ring"]["GBps"] == 800.0
+    assert s["default"]["fused_frac_all_ranks"] == 0.7
+    line["schedules"]["read_grid"] = sched(1400.0, order="FAILED: element 3")
+    assert not bench.summarize_proxy(line, 2, 0)["ok"]
+    assert not bench.summarize_proxy({"error": "boom"}, 2, 1)["ok"]
+    assert not bench.summarize_proxy({"config": {"algo": "read"}, "schedules": {"ring": sched(1.0)}}, 2, 0)["ok"]
