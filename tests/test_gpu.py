@@ -995,3 +995,21 @@ def test_reference_programs_against_this_abi(dev, prog):
             assert time.time() - t0 < 60, time.time() - t0
         rows = [ln for ln in outs[0][1].splitlines() if ln.strip() and ln.strip()[0].isdigit()]
         assert len(rows) == 2 and not any("FAIL" in ln for ln in rows), outs[0][1]
+
+
+def test_bench_self_launch_two_ranks(dev):
+    # `python3 bench.py --gpus 2` with no launcher starts its two rank processes
+    # itself (here on GPU 0: --same-device) and prints ONE line -- rank 0's -- with n_gpus 2 and
+    # every timed schedule's order-sensitive check ok
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(GW.ROOT, "bench.py"), "--gpus", "2", "--same-device", "--no-sweep",
+                        "--no-cpu-baseline", "--core-only", "--count", str(16 << 20), "--steps", "5", "--warmup", "2"],
+                       capture_output=True, text=True, timeout=280, env=env, cwd=GW.ROOT)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert r.returncode == 0 and len(lines) == 1, (r.returncode, r.stdout[-500:], r.stderr[-2000:])
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["result_check"] == "ok", d
+    assert {s["verify"]["order_sensitive"] for s in d["schedules"].values()} == {"ok"}, d["schedules"]
