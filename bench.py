@@ -1530,7 +1530,7 @@ def main():
         guard.daemon = True
         guard.start()
         t_guard = time.time()
-    if n > 1 and not args.no_alt:
+    if n > 1 and not args.no_alt and not args.core_only:
         # the comparison ceiling: RCCL's all-reduce on the same buffer (torch.distributed nccl)
         pg = None
         if rank == 0:
