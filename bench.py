@@ -796,6 +796,23 @@ def free_port():
     return port
 
 
+def die_with_parent():
+    """In a rank process spawn_ranks started (MNCCL_BENCH_PARENT = the launcher's pid), before it
+    touches the GPU: SIGTERM when the launcher dies (PR_SET_PDEATHSIG), so no rank outlives a killed
+    bench.py; a launcher already gone by then ends the rank at once."""
+    ppid = os.environ.get("MNCCL_BENCH_PARENT")
+    if not ppid:
+        return
+    import ctypes
+    import signal
+    try:
+        ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGTERM), 0, 0, 0)  # PR_SET_PDEATHSIG = 1
+    except Exception:
+        return
+    if os.getppid() != int(ppid):
+        os._exit(1)
+
+
 def spawn_ranks(argv, n, env=None, timeout=None, grace=30.0):
     """Starts n rank processes of `argv`, one per GPU as the reference's perf_test runs one process
     per rank (tests/perf_test.cpp:34-49): RANK = LOCAL_RANK = r, WORLD_SIZE = n, MASTER_ADDR
@@ -811,8 +828,17 @@ def spawn_ranks(argv, n, env=None, timeout=None, grace=30.0):
     procs = []
     for r in range(n):
         e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
-                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MNCCL_BENCH_PARENT=str(os.getpid()))
         procs.append(subprocess.Popen(argv, env=e, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    # a launcher that stops this process (SIGTERM at its time limit) stops the ranks too
+    import signal
+
+    def stop(signum, frame):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        raise SystemExit(128 + signum)
+    old_term = signal.signal(signal.SIGTERM, stop) if threading.current_thread() is threading.main_thread() else None
     out = []
     reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
     reader.start()
@@ -839,6 +865,8 @@ def spawn_ranks(argv, n, env=None, timeout=None, grace=30.0):
             break
         time.sleep(0.1)
     reader.join(10)
+    if old_term is not None:
+        signal.signal(signal.SIGTERM, old_term)
     lines = [ln for ln in (out[0] if out else b"").decode(errors="replace").splitlines() if ln.strip()]
     rc = first_rc or next((p.returncode for p in procs if p.returncode != 0), 0)
     return rc, (lines[-1] if lines else None)
@@ -908,6 +936,7 @@ def proxy_allreduce(budget_s=150.0):
 
 
 def main():
+    die_with_parent()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=20)   # perf_test.cpp:93-99: 20 timed

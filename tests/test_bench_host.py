@@ -270,3 +270,43 @@ def test_summarize_proxy_line():
     assert not bench.summarize_proxy(line, 2, 0)["ok"]
     assert not bench.summarize_proxy({"error": "boom"}, 2, 1)["ok"]
     assert not bench.summarize_proxy({"config": {"algo": "read"}, "schedules": {"ring": sched(1.0)}}, 2, 0)["ok"]
+
+
+def test_spawned_ranks_die_with_a_killed_launcher(tmp_path):
+    # a launcher stopped at its time limit (SIGKILL: no handler runs) must not leave rank processes
+    # behind holding the GPU: every rank gets SIGTERM from the kernel when its parent dies
+    import signal
+    import time
+    pidfile = tmp_path / "pids"
+    child = ("import os, sys, time\n"
+             f"sys.path.insert(0, {ROOT!r})\n"
+             "import bench\n"
+             "bench.die_with_parent()\n"  # what bench.py's main() does first
+             f"open({str(pidfile)!r}, 'a').write(str(os.getpid()) + '\\n')\n"
+             "time.sleep(120)\n")
+    parent = ("import sys\n"
+              f"sys.path.insert(0, {ROOT!r})\n"
+              "import bench\n"
+              f"bench.spawn_ranks([sys.executable, '-c', {child!r}], 2, timeout=100)\n")
+    p = subprocess.Popen([sys.executable, "-c", parent])
+    for _ in range(200):
+        if pidfile.exists() and len(pidfile.read_text().split()) == 2:
+            break
+        time.sleep(0.05)
+    pids = [int(x) for x in pidfile.read_text().split()]
+    os.kill(p.pid, signal.SIGKILL)
+    p.wait()
+    deadline = time.time() + 10
+    alive = pids
+    while alive and time.time() < deadline:
+        alive = []
+        for pid in pids:
+            try:
+                os.kill(pid, 0)
+                st = open(f"/proc/{pid}/stat").read().split()[2]
+                if st != "Z":
+                    alive.append(pid)
+            except (ProcessLookupError, FileNotFoundError):
+                pass
+        time.sleep(0.1)
+    assert not alive, f"rank processes {alive} outlived their launcher"
