@@ -41,7 +41,7 @@ def load():
     return _lib
 
 
-# schedules: the ring, the one-shot, read in its push form, read in its load form, read's grid form
+# schedules: the ring, the one-shot, read (the persistent kernel), read's grid form
 RING, ONESHOT, READ, READ_GRID = 0, 1, 2, 4  # (3: the load form, removed in 6.0)
 
 

@@ -76,7 +76,7 @@ def main():
                 "dispatches": [len(fe), len(wr)],
                 "note": f"{n} ranks sharing ONE MI355X (proxy); rank 0 profiled (apps/bin/perf_test --sizes 1024, "
                         "default knobs); medians after the first 5 dispatches; fused bytes = 4 B x chunk x (6n-4) for "
-                        "the ring, x 2n for read's push form, x (3n-1) for its load form",
+                        "the ring, x 2n for the read schedule (either form)",
                 "source": f"profiles/{rnd}_proxy_pmc_n{n}.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate "
                           "passes; FETCH x2, KiB x1024)",
             }
