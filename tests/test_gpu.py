@@ -413,13 +413,14 @@ def test_registered_windows_parity(dev, n):
         assert o["info"]["read_map_failures"] == 0 and o["info"]["ipc_open_failures"] == 0
 
 
-def test_registered_windows_auto_rendezvous(dev):
-    # MINI_NCCL_WINDOW_RENDEZVOUS unset (auto): window calls skip the host rendezvous only when no
-    # two ranks share a GPU; co-located ranks negotiate them like any other call (they meet faster
-    # on the host: profiles/r6_small_calls_windows.txt) -- the same bits either way
+@pytest.mark.parametrize("knob", ["-1", "1"])
+def test_registered_windows_auto_rendezvous(dev, knob):
+    # MINI_NCCL_WINDOW_RENDEZVOUS unset (-1, auto): window calls skip the host rendezvous only when
+    # no two ranks share a GPU; co-located ranks negotiate them like any other call (they meet faster
+    # on the host: profiles/r6_small_calls_windows.txt); 1: always negotiated -- the same bits
     n = 3
-    out = _run_windows(n, "parity", {"MINI_NCCL_WINDOW_RENDEZVOUS": "-1"}, timeout=600)
-    shared = any(out[r]["info"]["ranks_on_device"] > 1 for r in range(n))
+    out = _run_windows(n, "parity", {"MINI_NCCL_WINDOW_RENDEZVOUS": knob}, timeout=600)
+    shared = knob == "1" or any(out[r]["info"]["ranks_on_device"] > 1 for r in range(n))
     for r in range(n):
         o = out[r]
         assert all(rc == 0 for rc in o["rcs"]) and all(b == 0 for b in o["bad"]), (r, o["rcs"], o["bad"])
