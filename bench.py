@@ -825,6 +825,8 @@ def spawn_ranks(argv, n, env=None, timeout=None, grace=30.0):
     import subprocess
     port = free_port()
     base = dict(os.environ if env is None else env)
+    # the library's own bootstrap port (bench.py defaults it to MASTER_PORT + 7): a free one too
+    base.setdefault("MINI_NCCL_PORT", str(free_port()))
     procs = []
     for r in range(n):
         e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
