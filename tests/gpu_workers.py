@@ -681,6 +681,57 @@ def huge_rank(rank, n, port, env, count, out_q):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def far_offsets_rank(rank, n, port, env, count, algos, out_q):
+    """Chunks beyond 4 GiB (byte offsets past 2^32 in every kernel's addressing, 288 GB of HBM per
+    GPU): int32 x_r[i] = uint32(i) * (r + 1), wrapping, so every element's value names its position
+    up to 2^32 elements -- a 32-bit wrap of a byte offset reads another position's value.  Filled and
+    checked on the device (testkern.hip: 8 GiB per rank is too much for a host-side check).  Out of
+    place, one call per schedule, the whole recv checked each time: body = the sum over ranks
+    (n(n+1)/2 * i, wrapping), tail = this rank's own input."""
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import ctypes
+        import hip_rt
+        import mini_nccl as M
+        use_rank_device(rank)
+        K = testkern()
+        comm = M.Comm(n, rank, "127.0.0.1")
+        send = hip_rt.DeviceBuffer(count * 4)
+        recv = hip_rt.DeviceBuffer(count * 4)
+        res_buf = hip_rt.DeviceBuffer(256)
+        vp = ctypes.c_void_p
+        hip_rt.check(K.mnccl_test_iota(vp(send.ptr), count, rank + 1, None), "iota")
+        hip_rt.sync()
+        body = (count // n) * n
+
+        def check(buf, mult_body, mult_tail):
+            hip_rt.check(K.mnccl_test_check_iota(vp(buf.ptr), count, body, mult_body, mult_tail, vp(res_buf.ptr),
+                                                 None), "check")
+            hip_rt.sync()
+            bad, first = (int(v) for v in res_buf.download(np.uint64, 2))
+            return bad, (first if bad else -1)
+
+        # the checker itself: my input is not the sum, so it must flag the body from element 1 on
+        checker = check(send, n * (n + 1) // 2, rank + 1)
+        res = []
+        for algo in algos:
+            recv.fill_byte(0xA5)
+            comm.set_algo(algo)
+            rc = comm.all_reduce(send.ptr, recv.ptr, count, M.ncclInt32, M.ncclSum, 0)
+            hip_rt.sync()
+            bad, first = check(recv, n * (n + 1) // 2, rank + 1)
+            ci = comm.info()
+            res.append({"algo": algo, "rc": rc, "bad": bad, "first": first,
+                        "last_algo": ci["last_algo"], "grid_calls": ci["read_grid_calls"]})
+        send.free()
+        recv.free()
+        res_buf.free()
+        out_q.put((rank, {"results": res, "checker": checker, "body": body, "destroy": comm.destroy()}))
+    except Exception:
+        out_q.put((rank, {"error": traceback.format_exc()}))
+
+
 def destroy_inflight_rank(rank, n, port, env, out_q):
     """Stream-ordered calls still running when ncclCommDestroy is called: destroy waits for
     them (their kernels write into the peers' memory, which the peers free right after), and
@@ -835,12 +886,15 @@ def local_reduce_in_place_large():
 
 
 def testkern():
-    """tests/lib/libmnccl_testkern.so: plain-load consumer kernels (test infrastructure)."""
+    """tests/lib/libmnccl_testkern.so: plain-load consumer kernels and the position-coded fill /
+    check (test infrastructure)."""
     import ctypes
     L = ctypes.CDLL(os.path.join(HERE, "lib", "libmnccl_testkern.so"))
     vp, u64 = ctypes.c_void_p, ctypes.c_uint64
     L.mnccl_test_touch.argtypes = [vp, u64, vp, vp]
     L.mnccl_test_copy.argtypes = [vp, vp, u64, vp]
+    L.mnccl_test_iota.argtypes = [vp, u64, ctypes.c_uint32, vp]
+    L.mnccl_test_check_iota.argtypes = [vp, u64, u64, ctypes.c_uint32, ctypes.c_uint32, vp, vp]
     return L
 
 

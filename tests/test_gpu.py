@@ -945,6 +945,28 @@ def test_count_beyond_int32(dev):
         assert out[r]["rc"] == 0 and out[r]["bad"] == 0, out[r]
 
 
+def test_chunks_beyond_4gib(dev):
+    # 2 ranks, 2^31 + 2^20 + 9 int32 per rank (8 GiB + 4 MiB): rank 1's chunk starts past 2^32
+    # bytes; position-coded values (far_offsets_rank) catch a wrapped offset in any schedule
+    port = GW.free_port()
+    count = (1 << 31) + (1 << 20) + 9
+    algos = [0, 2, 4]  # ring, read (persistent), read's grid form
+    env = {"MINI_NCCL_TIMEOUT_MS": "60000", "GPU_MAX_HW_QUEUES": "2"}
+    out = GW.run_ranks(GW.far_offsets_rank, 2, lambda r: (r, 2, port, env, count, algos), 900)
+    assert sorted(out) == [0, 1], out
+    for r in range(2):
+        assert "error" not in out[r], out[r]["error"]
+        bad, first = out[r]["checker"]  # the device check flags an input that is not the sum
+        assert first == 1 and bad >= out[r]["body"] - 2, out[r]
+        res = out[r]["results"]
+        assert [x["algo"] for x in res] == algos, res
+        for x in res:
+            assert x["rc"] == 0 and x["bad"] == 0, (r, x)
+        assert [x["last_algo"] for x in res][:2] == [0, 2], res
+        assert res[2]["grid_calls"] == res[1]["grid_calls"] + 1, res  # the grid form ran
+        assert out[r]["destroy"] == 0, out[r]
+
+
 def _run_procs(cmds, env, timeout):
     import subprocess
     procs = [subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env) for c in cmds]
