@@ -732,6 +732,70 @@ def far_offsets_rank(rank, n, port, env, count, algos, out_q):
         out_q.put((rank, {"error": traceback.format_exc()}))
 
 
+def threaded_ranks_proc(n, port, env, cases, out_q):
+    """n ranks as threads of ONE process, all on this GPU: the library's same-process peer paths
+    (comm.cpp exchange_and_map: raw pointers for scratch / mailbox; peerbuf.cpp: the peers' user
+    buffers in this address space, no dma-buf) instead of IPC.  Each rank thread has its own
+    non-blocking stream; every allocation, upload, memset and free happens between barriers while
+    no all-reduce kernel runs (a device-wide synchronisation would otherwise wait for another
+    thread's kernel, which waits for this thread's).  Each case is checked bit-exact against the
+    oracle.  Reports {rank: results}."""
+    import threading
+    try:
+        os.environ.update(env)
+        os.environ["MINI_NCCL_PORT"] = str(port)
+        import hip_rt
+        import mini_nccl as M
+        import oracle_api as O
+        bar = threading.Barrier(n)
+        out = {}
+
+        def rank_main(r):
+            try:
+                hip_rt.set_device(0)
+                comm = M.Comm(n, r, "127.0.0.1")
+                st = hip_rt.Stream()
+                res = []
+                for case in cases:
+                    dtype, count, algo, inplace = case["dtype"], case["count"], case["algo"], case["inplace"]
+                    xs = make_inputs(n, count, dtype, case["seed"], False)
+                    exp = O.allreduce(xs, dtype, "sum", inplace=inplace)[r]
+                    code, npd = O.DTYPES[dtype]
+                    send = hip_rt.DeviceBuffer(xs[r].nbytes)
+                    recv = send if inplace else hip_rt.DeviceBuffer(xs[r].nbytes)
+                    send.upload(xs[r])
+                    if not inplace:
+                        recv.fill_byte(0xAB)
+                    comm.set_algo(algo)
+                    bar.wait(120)  # every thread prepared: no memset / copy / free from here on
+                    rc = comm.all_reduce(send.ptr, recv.ptr, count, code, M.ncclSum, st.handle)
+                    st.sync()
+                    bar.wait(120)  # every thread's kernel done
+                    bad, first = compare(recv.download(npd, count), exp, dtype, True)
+                    res.append({"case": case, "rc": rc, "bad": bad, "first": first,
+                                "last_algo": comm.info()["last_algo"]})
+                    if recv is not send:
+                        recv.free()
+                    send.free()
+                    bar.wait(120)  # frees done before anyone's next call
+                info = comm.info()
+                st.destroy()
+                out[r] = {"results": res, "ranks_on_device": info["ranks_on_device"],
+                          "ipc_open_failures": info["ipc_open_failures"], "destroy": comm.destroy()}
+            except Exception:
+                out[r] = {"error": traceback.format_exc()}
+                bar.abort()
+
+        ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(n)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        out_q.put((0, {"ranks": out}))
+    except Exception:
+        out_q.put((0, {"error": traceback.format_exc()}))
+
+
 def destroy_inflight_rank(rank, n, port, env, out_q):
     """Stream-ordered calls still running when ncclCommDestroy is called: destroy waits for
     them (their kernels write into the peers' memory, which the peers free right after), and

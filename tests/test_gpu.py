@@ -967,6 +967,32 @@ def test_chunks_beyond_4gib(dev):
         assert out[r]["destroy"] == 0, out[r]
 
 
+@pytest.mark.parametrize("n", [2, 3])
+def test_ranks_as_threads_of_one_process(dev, n):
+    # the same-process peer paths (raw pointers, no IPC) under every schedule, bit-exact
+    port = GW.free_port()
+    cases = [dict(dtype="f32", count=1000, algo=-1, inplace=False, seed=61),          # auto: small call
+             dict(dtype="f32", count=(1 << 20) + 3, algo=0, inplace=False, seed=62),  # ring
+             dict(dtype="f32", count=(1 << 20) + 3, algo=2, inplace=True, seed=63),   # read, persistent
+             dict(dtype="f32", count=3 << 21, algo=4, inplace=False, seed=64),        # read, grid form
+             dict(dtype="bf16", count=3 << 21, algo=-1, inplace=False, seed=65),      # auto, large
+             dict(dtype="f64", count=4099, algo=3, inplace=False, seed=66)]           # one-shot
+    env = {"MINI_NCCL_TIMEOUT_MS": "30000"}
+    out = GW.run_ranks(GW.threaded_ranks_proc, 1, lambda _: (n, port, env, cases), 300)
+    assert 0 in out and "error" not in out[0], out
+    ranks = out[0]["ranks"]
+    assert sorted(ranks) == list(range(n)), ranks
+    for r in range(n):
+        o = ranks[r]
+        assert "error" not in o, o["error"]
+        assert o["ranks_on_device"] == n and o["ipc_open_failures"] == 0 and o["destroy"] == 0, o
+        assert len(o["results"]) == len(cases), o
+        for x in o["results"]:
+            assert x["rc"] == 0 and x["bad"] == 0, (r, x)
+        algos = [x["last_algo"] for x in o["results"]]
+        assert algos[1] == 0 and algos[2] == 2 and algos[5] == 3, algos
+
+
 def _run_procs(cmds, env, timeout):
     import subprocess
     procs = [subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env) for c in cmds]
