@@ -749,6 +749,11 @@ def threaded_ranks_proc(n, port, env, cases, out_q):
         import oracle_api as O
         bar = threading.Barrier(n)
         out = {}
+        # inputs and the oracle's outputs once per case, shared by the rank threads
+        prepared = []
+        for case in cases:
+            xs = make_inputs(n, case["count"], case["dtype"], case["seed"], False)
+            prepared.append((xs, O.allreduce(xs, case["dtype"], "sum", inplace=case["inplace"])))
 
         def rank_main(r):
             try:
@@ -756,10 +761,9 @@ def threaded_ranks_proc(n, port, env, cases, out_q):
                 comm = M.Comm(n, r, "127.0.0.1")
                 st = hip_rt.Stream()
                 res = []
-                for case in cases:
+                for case, (xs, outs) in zip(cases, prepared):
                     dtype, count, algo, inplace = case["dtype"], case["count"], case["algo"], case["inplace"]
-                    xs = make_inputs(n, count, dtype, case["seed"], False)
-                    exp = O.allreduce(xs, dtype, "sum", inplace=inplace)[r]
+                    exp = outs[r]
                     code, npd = O.DTYPES[dtype]
                     send = hip_rt.DeviceBuffer(xs[r].nbytes)
                     recv = send if inplace else hip_rt.DeviceBuffer(xs[r].nbytes)

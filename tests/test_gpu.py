@@ -993,6 +993,31 @@ def test_ranks_as_threads_of_one_process(dev, n):
         assert algos[1] == 0 and algos[2] == 2 and algos[5] == 3, algos
 
 
+def test_sixteen_ranks_as_threads(dev):
+    # the largest communicator (kMaxRanks = 16) on the GPU: 16 rank threads of one process (16
+    # rank PROCESSES would exceed the box's GPU process limit), one hardware queue per rank's
+    # stream so every rank's persistent kernel is resident at once
+    port = GW.free_port()
+    cases = [dict(dtype="f32", count=(1 << 20) + 5, algo=2, inplace=False, seed=71),   # read
+             dict(dtype="f32", count=(1 << 20) + 5, algo=0, inplace=True, seed=72),    # ring
+             dict(dtype="bf16", count=4 << 20, algo=-1, inplace=False, seed=73),       # auto, large
+             dict(dtype="i32", count=16 * 7 + 3, algo=-1, inplace=False, seed=74),     # auto, tiny
+             dict(dtype="f64", count=999, algo=3, inplace=False, seed=75)]             # one-shot
+    env = {"MINI_NCCL_TIMEOUT_MS": "60000", "GPU_MAX_HW_QUEUES": "16"}
+    out = GW.run_ranks(GW.threaded_ranks_proc, 1, lambda _: (16, port, env, cases), 300)
+    assert 0 in out and "error" not in out[0], out
+    ranks = out[0]["ranks"]
+    assert sorted(ranks) == list(range(16)), ranks
+    for r in range(16):
+        o = ranks[r]
+        assert "error" not in o, o["error"]
+        assert o["ranks_on_device"] == 16 and o["destroy"] == 0, o
+        for x in o["results"]:
+            assert x["rc"] == 0 and x["bad"] == 0, (r, x)
+        algos = [x["last_algo"] for x in o["results"]]
+        assert algos[0] == 2 and algos[1] == 0 and algos[4] == 3, algos
+
+
 def _run_procs(cmds, env, timeout):
     import subprocess
     procs = [subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env) for c in cmds]
